@@ -1,0 +1,123 @@
+/* zchunk.h -- C ABI of the MI355X rolling-hash chunking engine (libzchunk.so).
+ *
+ * Drop-in for the inner loop of zbackup's BackupCreator: a byte stream goes
+ * in, the backup instruction records come out, bit-exact with
+ * /root/reference/backup_creator.cc for the same bytes, chunk.max_size and
+ * index contents.  Plain C types only; every call returns an int status
+ * (ZC_OK == 0, negative on error; zc_last_error() has the message).  One
+ * context per stream per GPU; a context is not shared between threads.
+ *
+ * Reference interfaces each entry point replaces:
+ *   zc_create              BackupCreator::BackupCreator(Config const &, ChunkIndex &,
+ *                          ChunkStorage::Writer &)        backup_creator.hh:83 / .cc:18-38
+ *                          (chunk.max_size = W: zbackup.proto:79, config.cc:266-282)
+ *   zc_seed_index          ChunkIndex::loadIndex -> registerNewChunkId, the static
+ *                          probe set of an existing repository   chunk_index.cc:26-79,163-182
+ *   zc_get_input_buffer    BackupCreator::getInputBuffer()       backup_creator.hh:78 / .cc:40-43
+ *   zc_get_input_buffer_size  BackupCreator::getInputBufferSize() backup_creator.hh:79 / .cc:45-54
+ *   zc_handle_more_data    BackupCreator::handleMoreData(unsigned) backup_creator.hh:81 / .cc:56-108
+ *   zc_finish              BackupCreator::finish()               backup_creator.hh:85 / .cc:147-172
+ *   zc_get_records         BackupCreator::getBackupData(string &) as structured records
+ *                          (one per BackupInstruction, zbackup.proto:149-159)
+ *                                                                backup_creator.hh:89 / .cc:275-280
+ *   zc_chunk_device        the same stream already resident in HBM (feed + finish in one call)
+ *   zc_last_error          the DEF_EX exceptions / CHECK aborts of the reference
+ *                          (backup_creator.cc:112,165-166, chunk_index.hh:88-89)
+ */
+#ifndef ZCHUNK_H
+#define ZCHUNK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZCHUNK_ABI_VERSION 1
+
+enum zc_status {
+  ZC_OK = 0,
+  ZC_ERR_ARG = -1,      /* bad argument (null pointer, W == 0, misaligned device buffer) */
+  ZC_ERR_HIP = -2,      /* HIP runtime error (message in zc_last_error) */
+  ZC_ERR_NOMEM = -3,    /* device or host allocation failed */
+  ZC_ERR_STATE = -4     /* call out of order (e.g. feeding after zc_finish) */
+};
+
+/* context flags */
+enum {
+  ZC_FLAG_SHA1 = 1u,     /* compute the SHA-1 half of every chunk id (ChunkId::cryptoHash)
+                            and register the stream's new chunks in the context's index,
+                            so a later stream on the same context can match them */
+  ZC_FLAG_TIMING = 2u    /* record per-stage device timings (zc_get_stats) */
+};
+
+/* record kinds: chunk_to_emit of a chunk cut and saved by this stream (NEW),
+ * chunk_to_emit of a window matched in the index (DUP), bytes_to_emit (BYTES,
+ * fragments under 128 bytes; the bytes are the caller's [offset, offset+size)) */
+enum { ZC_CHUNK_NEW = 0, ZC_CHUNK_DUP = 1, ZC_BYTES = 2 };
+
+typedef struct {
+  uint64_t offset;   /* stream offset of the first byte the instruction covers */
+  uint32_t size;     /* bytes covered */
+  uint32_t kind;     /* ZC_CHUNK_NEW / ZC_CHUNK_DUP / ZC_BYTES */
+  uint64_t rolling;  /* ChunkId::rollingHash (RollingHash digest); 0 for BYTES */
+  uint8_t sha1[16];  /* ChunkId::cryptoHash (SHA-1 prefix) if ZC_FLAG_SHA1, else 0 */
+} zc_record;
+
+/* one entry of an existing index: a ChunkId and the chunk size */
+typedef struct {
+  uint8_t sha1[16];
+  uint64_t rolling;
+  uint32_t size;
+  uint32_t reserved;
+} zc_seed;
+
+typedef struct {
+  double scan_ms;        /* zc_scan kernel (HIP events on the context stream) */
+  double resolve_ms;     /* everything after the scan, wall clock */
+  double total_ms;       /* whole call, wall clock */
+  uint64_t bytes;        /* stream length */
+  uint64_t anchors;      /* content anchors found by the scan */
+  uint64_t candidates;   /* anchor-probe candidates */
+  uint64_t epochs;       /* resolution epochs (1 + grid-shifting matches) */
+  uint64_t fscan_runs;   /* screen-hit runs from the exact-hash screen */
+} zc_stats;
+
+typedef struct zc_ctx zc_ctx;
+
+int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags);
+int zc_destroy(zc_ctx* ctx);
+int zc_seed_index(zc_ctx* ctx, const zc_seed* seeds, size_t n);
+
+/* host feed (zero-copy contract of BackupCreator: fill getInputBuffer() with up
+ * to getInputBufferSize() bytes, then report how many were written) */
+void* zc_get_input_buffer(zc_ctx* ctx);
+size_t zc_get_input_buffer_size(zc_ctx* ctx);
+int zc_handle_more_data(zc_ctx* ctx, size_t added);
+int zc_feed(zc_ctx* ctx, const void* host, size_t n); /* copying convenience form */
+int zc_finish(zc_ctx* ctx);
+
+/* device-resident stream: d_data is a device pointer on the context's GPU,
+ * 16-byte aligned; the call runs the whole pipeline and fills the records */
+int zc_chunk_device(zc_ctx* ctx, const void* d_data, uint64_t n);
+
+size_t zc_record_count(const zc_ctx* ctx);
+int zc_get_records(const zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);
+int zc_get_stats(const zc_ctx* ctx, zc_stats* out);
+int zc_reset(zc_ctx* ctx); /* begin a new stream (the seeded index is kept) */
+/* copy bytes [offset, offset+n) of the last processed stream to host memory
+ * (the payload of BYTES records, for serializing bytes_to_emit) */
+int zc_read_stream(const zc_ctx* ctx, uint64_t offset, size_t n, void* host_out);
+const char* zc_last_error(const zc_ctx* ctx);
+
+/* synthetic seeded stream on the device (tests / benchmarks): byte k is byte
+ * k mod 8 of splitmix64 word k / 8, little-endian */
+int zc_fill_splitmix64(void* d_data, uint64_t n, uint64_t seed, int device);
+
+int zc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,223 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference-built golden fixtures.  Integer/byte work, so the bar is bit-exact:
+offsets, sizes, kinds, 64-bit rolling hashes and SHA-1 prefixes."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests import golden_io
+
+pytestmark = pytest.mark.gpu
+
+CASES = golden_io.case_names()
+W64 = 65536
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    from zbackup_amd import _build
+    _build.build()
+    oracle.build()
+    return torch
+
+
+def _case(name):
+    return golden_io.load_case(f"{golden_io.GOLDEN}/{name}.txt")
+
+
+def _run_host_feed(data, W, seeds=(), chunk=None, sha1=True):
+    from zbackup_amd import BackupCreator
+    with BackupCreator(W, seeds=seeds, sha1=sha1) as bc:
+        if chunk is None:
+            bc.feed(data)
+        else:
+            # the zero-copy contract of zutils.cc:100-124, in ragged pieces
+            rng = np.random.default_rng(len(data))
+            pos = 0
+            while pos < data.size:
+                buf = bc.get_input_buffer()
+                take = min(int(rng.integers(1, chunk + 1)), bc.get_input_buffer_size(), data.size - pos)
+                np.frombuffer(buf, dtype=np.uint8, count=take)[:] = data[pos:pos + take]
+                bc.handle_more_data(take)
+                pos += take
+        bc.finish()
+        return bc.record_tuples()
+
+
+def _run_device(torch, data, W, seeds=(), sha1=True):
+    from zbackup_amd import BackupCreator
+    t = torch.from_numpy(np.ascontiguousarray(data)).to("cuda") if data.size else torch.empty(
+        0, dtype=torch.uint8, device="cuda")
+    with BackupCreator(W, seeds=seeds, sha1=sha1) as bc:
+        bc.chunk_device(t.data_ptr(), data.size)
+        return bc.record_tuples()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_host_feed(torch_cuda, name):
+    meta, seeds, want = _case(name)
+    data = oracle.gen(meta["spec"])
+    assert _run_host_feed(data, meta["W"], seeds) == want
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_device_resident(torch_cuda, name):
+    meta, seeds, want = _case(name)
+    data = oracle.gen(meta["spec"])
+    assert _run_device(torch_cuda, data, meta["W"], seeds) == want
+
+
+@pytest.mark.parametrize("name", ["w4096_shift", "mixed", "frag50", "w257_periodic"])
+def test_ragged_feed(torch_cuda, name):
+    meta, seeds, want = _case(name)
+    data = oracle.gen(meta["spec"])
+    assert _run_host_feed(data, meta["W"], seeds, chunk=70001) == want
+
+
+# random stress: synthetic streams built from copies at arbitrary offsets,
+# zero runs and repeated bytes, checked against the oracle
+def _random_spec(rng, W):
+    segs, n = [], 0
+    for _ in range(int(rng.integers(2, 9))):
+        t = rng.integers(0, 5)
+        ln = int(rng.integers(1, 5 * W))
+        if t == 0 or n == 0:
+            segs.append(f"R{int(rng.integers(1, 1 << 30))}:{ln}")
+        elif t == 1:
+            segs.append(f"Z:{ln}")
+        elif t == 2:
+            segs.append(f"B{int(rng.integers(0, 256))}:{ln}")
+        else:
+            segs.append(f"C{int(rng.integers(0, n))}:{ln}")
+        n += ln
+    return ",".join(segs)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_streams_vs_oracle(torch_cuda, seed):
+    rng = np.random.default_rng(1000 + seed)
+    W = int(rng.choice([128, 200, 257, 1000, 1024, 4096, 4097, 65536]))
+    spec = _random_spec(rng, W)
+    data = oracle.gen(spec)
+    want = oracle.chunk(data, W)
+    assert _run_device(torch_cuda, data, W) == want, spec
+
+
+def test_index_persists_across_streams(torch_cuda):
+    # ChunkStorage::Writer::add -> ChunkIndex::addChunk: a second stream on the
+    # same context matches the first stream's chunks (zutils.cc:137-166 reuses
+    # one index for the iterative passes)
+    from zbackup_amd import BackupCreator
+    a = oracle.gen("R501:700000")
+    b = oracle.gen("R502:33333,R501:700000,R503:1000")
+    want_a = oracle.chunk(a, W64)
+    seeds = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in want_a if k == "N"]
+    want_b = oracle.chunk(b, W64, seeds=seeds)
+    assert sum(1 for r in want_b if r[0] == "D") > 0
+    with BackupCreator(W64, sha1=True) as bc:
+        bc.feed(a)
+        bc.finish()
+        assert bc.record_tuples() == want_a
+        bc.reset()
+        bc.feed(b)
+        bc.finish()
+        assert bc.record_tuples() == want_b
+
+
+def test_get_backup_data_matches_oracle_serialization(torch_cuda):
+    from zbackup_amd import BackupCreator, chunk_id_blob, serialize_instruction
+    meta, seeds, want = _case("frag50")
+    data = oracle.gen(meta["spec"])
+    expect = b""
+    for (k, off, size, h, sha) in want:
+        if k == "B":
+            expect += serialize_instruction(raw=data[off:off + size].tobytes())
+        else:
+            expect += serialize_instruction(chunk_blob=chunk_id_blob(bytes.fromhex(sha), h))
+    with BackupCreator(meta["W"]) as bc:
+        bc.feed(data)
+        bc.finish()
+        assert bc.get_backup_data() == expect
+        with pytest.raises(Exception):
+            bc.get_backup_data()  # backup_creator.cc:277 CHECK: only once
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 1000, 4099, 1 << 20])
+def test_device_filler_matches_oracle_generator(torch_cuda, n):
+    from zbackup_amd import fill_splitmix64
+    t = torch_cuda.empty(max(n, 1), dtype=torch_cuda.uint8, device="cuda")
+    fill_splitmix64(t.data_ptr(), n, 77)
+    assert np.array_equal(t.cpu().numpy()[:n], oracle.splitmix64(n, 77))
+
+
+# --- BASELINE.json configs at full size: size-independent properties --------
+
+def _sample_digests(torch, t, offsets, size):
+    host = t.cpu().numpy() if t.numel() <= (1 << 24) else None
+    out = []
+    for off in offsets:
+        chunk = host[off:off + size] if host is not None else t[off:off + size].cpu().numpy()
+        out.append(oracle.digest(chunk))
+    return out
+
+
+@pytest.fixture(scope="module")
+def big_random(torch_cuda):
+    from zbackup_amd import fill_splitmix64
+    n = 8 << 30
+    t = torch_cuda.empty(n, dtype=torch_cuda.uint8, device="cuda")
+    fill_splitmix64(t.data_ptr(), n, 2024)
+    yield t
+    del t
+    torch_cuda.cuda.empty_cache()
+
+
+def test_c2_random_8gib_grid(torch_cuda, big_random):
+    from zbackup_amd import BackupCreator
+    n = big_random.numel()
+    with BackupCreator(W64, sha1=False) as bc:
+        bc.chunk_device(big_random.data_ptr(), n)
+        recs = bc.records()
+    assert len(recs) == n // W64
+    assert (recs["kind"] == 0).all()
+    assert np.array_equal(recs["offset"], np.arange(n // W64, dtype=np.uint64) * W64)
+    assert (recs["size"] == W64).all()
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([[0, len(recs) - 1], rng.integers(0, len(recs), 254)]))
+    want = _sample_digests(torch_cuda, big_random, [int(recs["offset"][i]) for i in idx], W64)
+    assert [int(recs["rolling"][i]) for i in idx] == want
+
+
+def test_c3_half_duplicated_8gib(torch_cuda, big_random):
+    from zbackup_amd import BackupCreator
+    n = big_random.numel()
+    half = n // 2
+    big_random[half:].copy_(big_random[:half])
+    with BackupCreator(W64, sha1=False) as bc:
+        bc.chunk_device(big_random.data_ptr(), n)
+        recs = bc.records()
+    m = half // W64
+    assert len(recs) == 2 * m
+    assert (recs["kind"][:m] == 0).all() and (recs["kind"][m:] == 1).all()
+    assert np.array_equal(recs["rolling"][:m], recs["rolling"][m:])
+    assert np.array_equal(recs["offset"], np.arange(2 * m, dtype=np.uint64) * W64)
+    rng = np.random.default_rng(6)
+    idx = rng.integers(0, m, 64)
+    want = _sample_digests(torch_cuda, big_random, [int(recs["offset"][i]) for i in idx], W64)
+    assert [int(recs["rolling"][i]) for i in idx] == want
+
+
+def test_c5_all_zero_8gib(torch_cuda, big_random):
+    from zbackup_amd import BackupCreator
+    n = big_random.numel()
+    big_random.zero_()
+    with BackupCreator(W64, sha1=False) as bc:
+        bc.chunk_device(big_random.data_ptr(), n)
+        recs = bc.records()
+    assert len(recs) == n // W64
+    assert recs["kind"][0] == 0 and (recs["kind"][1:] == 1).all()
+    assert (recs["rolling"] == 0x172AEAFF81000001).all()
+    assert np.array_equal(recs["offset"], np.arange(n // W64, dtype=np.uint64) * W64)

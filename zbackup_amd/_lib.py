@@ -1,0 +1,80 @@
+"""ctypes binding of libzchunk.so (include/zchunk.h).
+
+The library is built in-tree (zbackup_amd/libzchunk.so).  Loading fails loudly
+if it is missing: there is no CPU fallback for the product path.
+"""
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libzchunk.so")
+
+ZC_OK, ZC_ERR_ARG, ZC_ERR_HIP, ZC_ERR_NOMEM, ZC_ERR_STATE = 0, -1, -2, -3, -4
+ZC_FLAG_SHA1, ZC_FLAG_TIMING = 1, 2
+ZC_CHUNK_NEW, ZC_CHUNK_DUP, ZC_BYTES = 0, 1, 2
+
+# every symbol include/zchunk.h declares
+EXPORTS = ["zc_create", "zc_destroy", "zc_seed_index", "zc_get_input_buffer",
+           "zc_get_input_buffer_size", "zc_handle_more_data", "zc_feed", "zc_finish",
+           "zc_chunk_device", "zc_record_count", "zc_get_records", "zc_get_stats", "zc_reset",
+           "zc_last_error", "zc_fill_splitmix64", "zc_abi_version", "zc_read_stream"]
+
+
+class ZcRecord(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("size", ctypes.c_uint32), ("kind", ctypes.c_uint32),
+                ("rolling", ctypes.c_uint64), ("sha1", ctypes.c_uint8 * 16)]
+
+
+class ZcSeed(ctypes.Structure):
+    _fields_ = [("sha1", ctypes.c_uint8 * 16), ("rolling", ctypes.c_uint64),
+                ("size", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class ZcStats(ctypes.Structure):
+    _fields_ = [("scan_ms", ctypes.c_double), ("resolve_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("bytes", ctypes.c_uint64),
+                ("anchors", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
+                ("epochs", ctypes.c_uint64), ("fscan_runs", ctypes.c_uint64)]
+
+
+class ZcError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libzchunk.so; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ZcError(f"{path} not built (run zbackup_amd/_build.py or __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    vp, u32, u64, sz, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int
+    sig = {
+        "zc_create": (i32, [ctypes.POINTER(vp), u32, i32, u32]),
+        "zc_destroy": (i32, [vp]),
+        "zc_seed_index": (i32, [vp, ctypes.POINTER(ZcSeed), sz]),
+        "zc_get_input_buffer": (vp, [vp]),
+        "zc_get_input_buffer_size": (sz, [vp]),
+        "zc_handle_more_data": (i32, [vp, sz]),
+        "zc_feed": (i32, [vp, vp, sz]),
+        "zc_finish": (i32, [vp]),
+        "zc_chunk_device": (i32, [vp, vp, u64]),
+        "zc_record_count": (sz, [vp]),
+        "zc_get_records": (i32, [vp, ctypes.POINTER(ZcRecord), sz, ctypes.POINTER(sz)]),
+        "zc_get_stats": (i32, [vp, ctypes.POINTER(ZcStats)]),
+        "zc_reset": (i32, [vp]),
+        "zc_last_error": (ctypes.c_char_p, [vp]),
+        "zc_fill_splitmix64": (i32, [vp, u64, u64, i32]),
+        "zc_abi_version": (i32, []),
+        "zc_read_stream": (i32, [vp, u64, sz, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L

@@ -1,0 +1,174 @@
+"""Python host mirror of zbackup's BackupCreator on the MI355X engine.
+
+Names, argument meaning and error behaviour follow the reference:
+  BackupCreator(config, chunkIndex, writer)      backup_creator.hh:83
+    getInputBuffer / getInputBufferSize          backup_creator.cc:40-54
+    handleMoreData(added)                        backup_creator.cc:56-108
+    finish()                                     backup_creator.cc:147-172
+    getBackupData(string &)  -- callable once    backup_creator.cc:275-280
+  ChunkId::toBlob  (16-byte SHA-1 prefix + LE rolling hash)   chunk_id.cc:19-27
+  Message::serialize (varint32 length + BackupInstruction)    message.cc:16-23
+
+All work runs in libzchunk.so on the GPU; there is no CPU fallback.
+"""
+import ctypes
+import struct
+
+import numpy as np
+
+from . import _lib
+
+RECORD_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u4"), ("kind", "<u4"),
+                         ("rolling", "<u8"), ("sha1", "u1", (16,))])
+KIND_CHAR = "NDB"
+
+
+def _check(L, ctx, rc, what):
+    if rc != _lib.ZC_OK:
+        msg = L.zc_last_error(ctx) if ctx else b""
+        raise _lib.ZcError(f"{what} failed ({rc}): {(msg or b'').decode(errors='replace')}")
+
+
+def chunk_id_blob(sha1_16, rolling):
+    """ChunkId::toBlob (chunk_id.cc:19-27)."""
+    return bytes(sha1_16) + struct.pack("<Q", rolling)
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def serialize_instruction(chunk_blob=None, raw=None):
+    """Message::serialize of one BackupInstruction (zbackup.proto:149-159)."""
+    body = b""
+    if chunk_blob is not None:
+        body += b"\x0a" + _varint(len(chunk_blob)) + chunk_blob
+    if raw is not None:
+        body += b"\x12" + _varint(len(raw)) + raw
+    return _varint(len(body)) + body
+
+
+class BackupCreator:
+    """One stream through the engine.  `seeds` are (sha1_16, rolling, size)
+    entries of an existing index (ChunkIndex::loadIndex)."""
+
+    def __init__(self, chunk_max_size=65536, seeds=(), device=0, sha1=True, timing=False):
+        self._L = _lib.load()
+        self.chunk_max_size = int(chunk_max_size)
+        flags = (_lib.ZC_FLAG_SHA1 if sha1 else 0) | (_lib.ZC_FLAG_TIMING if timing else 0)
+        ctx = ctypes.c_void_p()
+        rc = self._L.zc_create(ctypes.byref(ctx), self.chunk_max_size, device, flags)
+        if rc != _lib.ZC_OK:
+            raise _lib.ZcError(f"zc_create failed ({rc})")
+        self._ctx = ctx
+        self._data_taken = False
+        seeds = list(seeds)
+        if seeds:
+            arr = (_lib.ZcSeed * len(seeds))()
+            for i, (sha, rolling, size) in enumerate(seeds):
+                arr[i].sha1[:] = list(sha[:16])
+                arr[i].rolling = rolling
+                arr[i].size = size
+            _check(self._L, self._ctx, self._L.zc_seed_index(self._ctx, arr, len(seeds)), "zc_seed_index")
+
+    # -- feed contract -------------------------------------------------------
+    def get_input_buffer(self):
+        """Writable view of getInputBufferSize() bytes (pinned host staging)."""
+        p = self._L.zc_get_input_buffer(self._ctx)
+        if not p:
+            raise _lib.ZcError("no input buffer after finish()")
+        n = self._L.zc_get_input_buffer_size(self._ctx)
+        return (ctypes.c_uint8 * n).from_address(p)
+
+    def get_input_buffer_size(self):
+        return self._L.zc_get_input_buffer_size(self._ctx)
+
+    def handle_more_data(self, added):
+        _check(self._L, self._ctx, self._L.zc_handle_more_data(self._ctx, added), "handleMoreData")
+
+    def feed(self, data):
+        data = np.ascontiguousarray(np.frombuffer(memoryview(data), dtype=np.uint8))
+        _check(self._L, self._ctx, self._L.zc_feed(self._ctx, data.ctypes.data, data.size), "zc_feed")
+
+    def finish(self):
+        _check(self._L, self._ctx, self._L.zc_finish(self._ctx), "finish")
+
+    # -- device-resident stream ----------------------------------------------
+    def chunk_device(self, ptr, n):
+        """Process `n` bytes already in HBM at device pointer `ptr` (e.g. a torch
+        uint8 tensor's data_ptr()); feed + finish in one call."""
+        _check(self._L, self._ctx, self._L.zc_chunk_device(self._ctx, ctypes.c_void_p(ptr), n),
+               "zc_chunk_device")
+
+    # -- results -------------------------------------------------------------
+    def records(self):
+        n = self._L.zc_record_count(self._ctx)
+        out = np.zeros(n, dtype=RECORD_DTYPE)
+        got = ctypes.c_size_t()
+        _check(self._L, self._ctx,
+               self._L.zc_get_records(self._ctx, out.ctypes.data_as(ctypes.POINTER(_lib.ZcRecord)), n,
+                                      ctypes.byref(got)), "zc_get_records")
+        return out[: got.value]
+
+    def record_tuples(self):
+        """(kind_char, offset, size, rolling, sha1_hex) -- the oracle's format."""
+        return [(KIND_CHAR[r["kind"]], int(r["offset"]), int(r["size"]), int(r["rolling"]),
+                 bytes(r["sha1"]).hex()) for r in self.records()]
+
+    def read_stream(self, offset, n):
+        buf = np.empty(n, dtype=np.uint8)
+        _check(self._L, self._ctx, self._L.zc_read_stream(self._ctx, offset, n, buf.ctypes.data),
+               "zc_read_stream")
+        return buf.tobytes()
+
+    def get_backup_data(self):
+        """Serialized BackupInstruction stream; like the reference, only once."""
+        if self._data_taken:
+            raise _lib.ZcError("getBackupData() called twice")
+        self._data_taken = True
+        out = bytearray()
+        for r in self.records():
+            if r["kind"] == _lib.ZC_BYTES:
+                out += serialize_instruction(raw=self.read_stream(int(r["offset"]), int(r["size"])))
+            else:
+                out += serialize_instruction(chunk_blob=chunk_id_blob(r["sha1"], int(r["rolling"])))
+        return bytes(out)
+
+    def stats(self):
+        st = _lib.ZcStats()
+        _check(self._L, self._ctx, self._L.zc_get_stats(self._ctx, ctypes.byref(st)), "zc_get_stats")
+        return {name: getattr(st, name) for name, _ in _lib.ZcStats._fields_}
+
+    def reset(self):
+        _check(self._L, self._ctx, self._L.zc_reset(self._ctx), "zc_reset")
+        self._data_taken = False
+
+    def close(self):
+        if self._ctx:
+            self._L.zc_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fill_splitmix64(ptr, n, seed, device=0):
+    """Seeded synthetic stream written straight into HBM (same bytes as the oracle's)."""
+    L = _lib.load()
+    rc = L.zc_fill_splitmix64(ctypes.c_void_p(ptr), n, seed, device)
+    if rc != _lib.ZC_OK:
+        raise _lib.ZcError(f"zc_fill_splitmix64 failed ({rc})")

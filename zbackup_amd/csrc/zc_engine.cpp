@@ -1,0 +1,955 @@
+// zc_engine.cpp -- host side of libzchunk: the C ABI (include/zchunk.h), device
+// buffer management and the boundary resolver.
+//
+// The resolver replays the state machine of /root/reference/backup_creator.cc
+// (fill phase, rotate phase, max-size cut, match, finish) over the candidate
+// lists the kernels produce, instead of over every byte:
+//
+//   * Grid chunks.  After a reset at r the reference cuts chunk k =
+//     [r+kW, r+(k+1)W) in the iteration whose probe is at p = r+(k+2)W-1
+//     (backup_creator.cc:89-93), so chunk k is visible to probes p >= its
+//     "vis" time r+(k+2)W-1 (chunk_storage.cc:31-46 adds it synchronously).
+//   * Matches.  A probe at p >= r+W-1 matches iff the window [p-W+1, p] has
+//     the rolling key and SHA-1 prefix of a visible index entry
+//     (chunk_index.cc:119-143).  Candidates come from the anchor probe
+//     (windows sharing a content anchor with a chunk, verified byte-exact on
+//     the GPU) and from the exact-hash screen (keys without an anchor, and the
+//     static index, verified by 64-bit key + bytes or SHA-1).
+//   * On a match at m: grid chunks with vis <= m are saved (NEW), the pending
+//     bytes [s, m-W+1) are flushed (NEW, or BYTES under 128 bytes:
+//     backup_creator.cc:110-145), the window is emitted (DUP) and r = m+1.
+//     If r stays on the same grid (r - r_epoch = 0 mod W) the epoch goes on;
+//     otherwise a new epoch recomputes the grid chunks from r.
+//   * Finish (backup_creator.cc:147-172): the pending bytes plus the ring,
+//     as one piece or as a W-byte chunk and the remainder.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/zchunk.h"
+#include "zc_device.h"
+
+using namespace zc;
+
+namespace {
+
+struct ZcError {
+  int code;
+  std::string msg;
+};
+
+#define HCK(x)                                                                         \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      throw ZcError{ZC_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)};       \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  void ensure(size_t n) {
+    if (n <= cap && p) return;
+    release();
+    size_t want = n ? n : 1;
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e != hipSuccess) {
+      p = nullptr;
+      throw ZcError{ZC_ERR_NOMEM, std::string("hipMalloc(") + std::to_string(want * sizeof(T)) +
+                                      "): " + hipGetErrorString(e)};
+    }
+    cap = want;
+  }
+};
+
+struct StaticEntry {
+  uint64_t key;
+  uint8_t sha[16];
+};
+
+constexpr uint64_t kInf = ~0ull;
+constexpr size_t kFeedChunk = 8u << 20;
+constexpr size_t kFBatchMax = 1u << 20;
+
+}  // namespace
+
+struct zc_ctx {
+  int device = 0;
+  uint32_t W = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+
+  // host feed
+  uint8_t* stage = nullptr;  // pinned staging for the zero-copy feed contract
+  DevBuf<uint8_t> d_stream;
+  uint64_t n_stream = 0;
+  bool finished = false;
+  const uint8_t* d_last = nullptr;  // the stream the records describe
+  uint64_t n_last = 0;
+
+  std::vector<StaticEntry> statics;  // seeded index entries of size W
+  std::vector<zc_record> recs;
+  zc_stats stats{};
+
+  // scratch
+  DevBuf<uint64_t> blk, tile_off, ftile_off;
+  DevBuf<uint32_t> tile_cnt, ftile_cnt;
+  DevBuf<Anchor> pool;
+  DevBuf<unsigned long long> counters;
+  DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
+  DevBuf<uint32_t> c_anc;
+  DevBuf<uint8_t> c_dead;
+  DevBuf<uint64_t> tkeys;
+  DevBuf<uint32_t> tvals;
+  DevBuf<Cand> cand;
+  DevBuf<uint64_t> va, vb, dout;
+  DevBuf<uint32_t> vlen;
+  DevBuf<uint8_t> vok, sha_out;
+  DevBuf<uint32_t> f32, fbits;
+  DevBuf<Run> runs;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    HCK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class T>
+void h2d(zc_ctx& c, T* dst, const T* src, size_t n) {
+  if (n) HCK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, c.stream));
+}
+template <class T>
+void d2h(zc_ctx& c, T* dst, const T* src, size_t n) {
+  if (n) HCK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyDeviceToHost, c.stream));
+}
+void sync(zc_ctx& c) { HCK(hipStreamSynchronize(c.stream)); }
+
+// ---------------------------------------------------------------------------
+class Resolver {
+ public:
+  Resolver(zc_ctx& c, const uint8_t* d, uint64_t n)
+      : c_(c), d_(d), n_(n), W_(c.W), indexable_(c.W >= 128) {}
+
+  void run() {
+    auto t0 = std::chrono::steady_clock::now();
+    c_.recs.clear();
+    c_.stats = zc_stats{};
+    c_.stats.bytes = n_;
+    if (n_ == 0) return;
+    scan();
+    auto t1 = std::chrono::steady_clock::now();
+    // static entries keyed by rolling hash
+    for (size_t i = 0; i < c_.statics.size(); ++i) smap_[c_.statics[i].key].push_back((uint32_t)i);
+    r_ = 0;
+    s_ = 0;
+    while (epoch()) {
+    }
+    finalize();
+    auto t2 = std::chrono::steady_clock::now();
+    c_.stats.resolve_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    c_.stats.total_ms = std::chrono::duration<double, std::milli>(t2 - t0).count();
+  }
+
+ private:
+  zc_ctx& c_;
+  const uint8_t* d_;
+  const uint64_t n_;
+  const uint32_t W_;
+  const bool indexable_;
+  uint64_t npool_ = 0;
+
+  // resolver state
+  uint64_t r_ = 0, s_ = 0, r_e_ = 0;
+
+  // refs = indexable W-byte chunks that can be matched: [0, nconf_) saved in
+  // earlier epochs, [nconf_, nconf_+nspec_) this epoch's grid chunks
+  std::vector<uint64_t> start_, key_, fp_, vis_;
+  std::vector<uint32_t> anc_;
+  std::vector<uint8_t> dead_;
+  uint32_t nconf_ = 0, nspec_ = 0;
+  uint64_t ks_ = 0;  // next grid chunk of this epoch to save
+
+  std::unordered_map<uint64_t, std::vector<uint32_t>> fmap_;  // key -> anchorless refs (start order)
+  std::unordered_map<uint64_t, std::vector<uint32_t>> smap_;  // key -> statics
+  std::vector<Run> runs_;
+  uint64_t f_min_vis_ = kInf;
+  bool has_f_ = false;
+
+  struct ACand {
+    uint64_t p;
+    uint32_t ref;
+  };
+  std::vector<ACand> acands_;
+
+  // F verification batch (positions ascending)
+  struct FBatch {
+    std::vector<uint64_t> pos, h;
+    std::vector<int64_t> vref;     // ref verified against, -1 none
+    std::vector<uint8_t> vok;      // content equal to vref
+    std::vector<uint8_t> sha;      // 20 bytes per position (statics only)
+    std::vector<uint8_t> has_sha;
+    size_t cur = 0;
+  } fb_;
+
+  struct Piece {
+    size_t rec;
+    uint64_t a, b;
+  };
+  std::vector<Piece> need_digest_;
+
+  // ---------------------------------------------------------------- scan
+  void scan() {
+    const uint64_t ntiles = (n_ + ZC_TILE - 1) / ZC_TILE;
+    const uint64_t nspans = (n_ + ZC_SPAN - 1) / ZC_SPAN;
+    c_.blk.ensure(nspans);
+    c_.tile_off.ensure(ntiles);
+    c_.tile_cnt.ensure(ntiles);
+    c_.counters.ensure(CNT_LAST);
+    uint64_t cap = std::max<uint64_t>(n_ / 512, 4096);
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      c_.pool.ensure(cap);
+      HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+      if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
+      HCK(launch_scan(d_, n_, c_.blk.p, c_.pool.p, c_.pool.cap, c_.tile_off.p, c_.tile_cnt.p,
+                      c_.counters.p, c_.stream));
+      if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
+      unsigned long long cnt[CNT_LAST];
+      d2h(c_, cnt, c_.counters.p, CNT_LAST);
+      sync(c_);
+      if (c_.flags & ZC_FLAG_TIMING) {
+        float ms = 0;
+        HCK(hipEventElapsedTime(&ms, c_.ev0, c_.ev1));
+        c_.stats.scan_ms = ms;
+      }
+      if (!(cnt[CNT_OVERFLOW] & 1)) {
+        npool_ = cnt[CNT_POOL];
+        c_.stats.anchors = npool_;
+        return;
+      }
+      cap = cnt[CNT_POOL] + cnt[CNT_POOL] / 8 + 4096;
+    }
+    throw ZcError{ZC_ERR_NOMEM, "anchor pool overflow persisted"};
+  }
+
+  // ---------------------------------------------------------------- epoch
+  bool epoch() {
+    c_.stats.epochs++;
+    r_e_ = r_;
+    s_ = r_;
+    ks_ = 0;
+    nspec_ = (n_ >= r_e_ + 2ull * W_) ? (uint32_t)((n_ - r_e_ - 2ull * W_) / W_ + 1) : 0;
+    const uint32_t nrefs_spec = indexable_ ? nspec_ : 0;
+    const uint32_t nref = nconf_ + nrefs_spec;
+    start_.resize(nref);
+    key_.resize(nref);
+    fp_.resize(nref);
+    vis_.resize(nref);
+    anc_.resize(nref);
+    dead_.assign(nref, 0);
+    for (uint32_t k = 0; k < nrefs_spec; ++k) {
+      start_[nconf_ + k] = r_e_ + (uint64_t)k * W_;
+      vis_[nconf_ + k] = start_[nconf_ + k] + 2ull * W_ - 1;
+    }
+    acands_.clear();
+    runs_.clear();
+    fmap_.clear();
+    fb_ = FBatch{};
+    has_f_ = false;
+    f_min_vis_ = kInf;
+    if (nref) {
+      c_.c_start.ensure(nref);
+      c_.c_key.ensure(nref);
+      c_.c_fp.ensure(nref);
+      c_.c_vis.ensure(nref);
+      c_.c_anc.ensure(nref);
+      c_.c_dead.ensure(nref);
+      h2d(c_, c_.c_start.p, start_.data(), nref);
+      h2d(c_, c_.c_key.p, key_.data(), nconf_);
+      h2d(c_, c_.c_fp.p, fp_.data(), nconf_);
+      h2d(c_, c_.c_anc.p, anc_.data(), nconf_);
+      h2d(c_, c_.c_vis.p, vis_.data(), nref);
+      h2d(c_, c_.c_dead.p, dead_.data(), nref);
+      HCK(launch_chunk_meta(d_, n_, c_.blk.p, c_.pool.p, c_.tile_off.p, c_.tile_cnt.p,
+                            c_.c_start.p + nconf_, nrefs_spec, W_, pow257(W_), c_.c_key.p + nconf_,
+                            c_.c_fp.p + nconf_, c_.c_anc.p + nconf_, c_.stream));
+      d2h(c_, key_.data() + nconf_, c_.c_key.p + nconf_, nrefs_spec);
+      d2h(c_, fp_.data() + nconf_, c_.c_fp.p + nconf_, nrefs_spec);
+      d2h(c_, anc_.data() + nconf_, c_.c_anc.p + nconf_, nrefs_spec);
+      sync(c_);
+      probe_anchors(nref);
+    }
+    // keys without an anchor, and the static index, go through the exact screen
+    for (uint32_t i = 0; i < nref; ++i)
+      if (anc_[i] == ZC_NO_ANCHOR) {
+        fmap_[key_[i]].push_back(i);
+        f_min_vis_ = std::min(f_min_vis_, vis_[i]);
+      }
+    if (!smap_.empty()) f_min_vis_ = 0;
+    if (!fmap_.empty() || !smap_.empty()) fscan();
+    return walk();
+  }
+
+  void probe_anchors(uint32_t nref) {
+    uint32_t nanc = 0;
+    for (uint32_t i = 0; i < nref; ++i) nanc += anc_[i] != ZC_NO_ANCHOR;
+    if (!nanc || !npool_) return;
+    uint32_t tbits = 10;
+    while ((1u << tbits) < 2u * nanc) ++tbits;
+    const uint32_t tsize = 1u << tbits;
+    c_.tkeys.ensure(tsize);
+    c_.tvals.ensure(tsize);
+    HCK(launch_table_clear(c_.tkeys.p, tsize, c_.stream));
+    HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_fp.p, c_.c_anc.p, nref, c_.stream));
+    uint64_t cap = std::max<uint64_t>(1u << 16, nanc);
+    unsigned long long cnt[CNT_LAST];
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      c_.cand.ensure(cap);
+      HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
+      HCK(launch_probe(c_.pool.p, npool_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_start.p, c_.c_anc.p,
+                       c_.c_vis.p, c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p,
+                       c_.stream));
+      d2h(c_, cnt, c_.counters.p, CNT_LAST);
+      sync(c_);
+      if (cnt[CNT_CAND] <= c_.cand.cap) break;
+      cap = cnt[CNT_CAND] + 1024;
+      if (attempt == 2) throw ZcError{ZC_ERR_NOMEM, "candidate buffer overflow persisted"};
+    }
+    const uint64_t nc = cnt[CNT_CAND];
+    c_.stats.candidates += nc;
+    if (!nc) return;
+    std::vector<Cand> hc(nc);
+    d2h(c_, hc.data(), c_.cand.p, nc);
+    sync(c_);
+    // byte-exact verification of every candidate window against its chunk
+    std::vector<uint64_t> wa(nc), ra(nc);
+    for (uint64_t i = 0; i < nc; ++i) {
+      wa[i] = hc[i].p - W_ + 1;
+      ra[i] = start_[hc[i].ref];
+    }
+    std::vector<uint8_t> ok = verify_pairs(wa, ra, W_);
+    acands_.reserve(nc);
+    for (uint64_t i = 0; i < nc; ++i)
+      if (ok[i]) acands_.push_back({hc[i].p, hc[i].ref});
+    std::sort(acands_.begin(), acands_.end(), [](const ACand& a, const ACand& b) {
+      return a.p != b.p ? a.p < b.p : a.ref < b.ref;
+    });
+  }
+
+  std::vector<uint8_t> verify_pairs(const std::vector<uint64_t>& wa, const std::vector<uint64_t>& ra,
+                                    uint32_t len) {
+    const size_t np = wa.size();
+    std::vector<uint8_t> ok(np, 0);
+    if (!np) return ok;
+    c_.va.ensure(np);
+    c_.vb.ensure(np);
+    c_.vok.ensure(np);
+    h2d(c_, c_.va.p, wa.data(), np);
+    h2d(c_, c_.vb.p, ra.data(), np);
+    HCK(launch_verify_pairs(d_, c_.va.p, c_.vb.p, len, (uint32_t)np, c_.vok.p, c_.stream));
+    d2h(c_, ok.data(), c_.vok.p, np);
+    sync(c_);
+    return ok;
+  }
+
+  std::vector<uint64_t> range_digests(const std::vector<uint64_t>& a, const std::vector<uint64_t>& b) {
+    const size_t nr = a.size();
+    std::vector<uint64_t> out(nr);
+    if (!nr) return out;
+    c_.va.ensure(nr);
+    c_.vb.ensure(nr);
+    c_.dout.ensure(nr);
+    h2d(c_, c_.va.p, a.data(), nr);
+    h2d(c_, c_.vb.p, b.data(), nr);
+    HCK(launch_range_digest(d_, n_, c_.blk.p, c_.va.p, c_.vb.p, (uint32_t)nr, c_.dout.p, c_.stream));
+    d2h(c_, out.data(), c_.dout.p, nr);
+    sync(c_);
+    return out;
+  }
+
+  std::vector<uint8_t> sha1s(const std::vector<uint64_t>& a, const std::vector<uint32_t>& len) {
+    const size_t nr = a.size();
+    std::vector<uint8_t> out(nr * 20);
+    if (!nr) return out;
+    c_.va.ensure(nr);
+    c_.vlen.ensure(nr);
+    c_.sha_out.ensure(nr * 20);
+    h2d(c_, c_.va.p, a.data(), nr);
+    h2d(c_, c_.vlen.p, len.data(), nr);
+    HCK(launch_sha1(d_, c_.va.p, c_.vlen.p, (uint32_t)nr, c_.sha_out.p, c_.stream));
+    d2h(c_, out.data(), c_.sha_out.p, nr * 20);
+    sync(c_);
+    return out;
+  }
+
+  // ---------------------------------------------------------------- F screen
+  void fscan() {
+    std::vector<uint32_t> keys32;
+    for (auto& kv : fmap_) keys32.push_back((uint32_t)kv.first);
+    for (auto& kv : smap_) keys32.push_back((uint32_t)kv.first);
+    std::sort(keys32.begin(), keys32.end());
+    keys32.erase(std::unique(keys32.begin(), keys32.end()), keys32.end());
+    const uint32_t nf = (uint32_t)keys32.size();
+    c_.f32.ensure(std::max<uint32_t>(nf, 1));
+    h2d(c_, c_.f32.p, keys32.data(), nf);
+    c_.fbits.ensure(1u << 14);
+    if (nf > 16) {
+      std::vector<uint32_t> bits(1u << 14, 0);
+      for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
+      h2d(c_, c_.fbits.p, bits.data(), bits.size());
+    }
+    const uint64_t p_start = r_e_ + W_ - 1;
+    if (p_start >= n_) return;
+    const uint64_t ntiles = (n_ + ZC_TILE - 1) / ZC_TILE;
+    c_.ftile_off.ensure(ntiles);
+    c_.ftile_cnt.ensure(ntiles);
+    uint64_t cap = std::max<uint64_t>(ntiles * 4, 1u << 16);
+    unsigned long long cnt[CNT_LAST];
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      c_.runs.ensure(cap);
+      HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+      HCK(launch_fscan(d_, n_, c_.blk.p, W_, (uint32_t)pow257(W_), p_start, c_.f32.p, nf, c_.fbits.p,
+                       c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
+      d2h(c_, cnt, c_.counters.p, CNT_LAST);
+      sync(c_);
+      if (!(cnt[CNT_OVERFLOW] & 2)) break;
+      cap = cnt[CNT_RUNS] + 1024;
+      if (attempt == 2) throw ZcError{ZC_ERR_NOMEM, "screen-run buffer overflow persisted"};
+    }
+    const uint64_t nruns = cnt[CNT_RUNS];
+    c_.stats.fscan_runs += nruns;
+    std::vector<Run> raw(nruns);
+    std::vector<uint64_t> toff(ntiles);
+    std::vector<uint32_t> tcnt(ntiles);
+    d2h(c_, raw.data(), c_.runs.p, nruns);
+    d2h(c_, toff.data(), c_.ftile_off.p, ntiles);
+    d2h(c_, tcnt.data(), c_.ftile_cnt.p, ntiles);
+    sync(c_);
+    for (uint64_t t = 0; t < ntiles; ++t)
+      for (uint32_t i = 0; i < tcnt[t]; ++i) {
+        const Run& q = raw[toff[t] + i];
+        if (!runs_.empty() && runs_.back().end == q.start)
+          runs_.back().end = q.end;
+        else
+          runs_.push_back(q);
+      }
+    has_f_ = !runs_.empty();
+  }
+
+  // first position p >= from inside the screen runs, or kInf
+  size_t irun_ = 0;
+  uint64_t next_run_pos(uint64_t from) {
+    while (irun_ < runs_.size() && runs_[irun_].end <= from) ++irun_;
+    if (irun_ == runs_.size()) return kInf;
+    return std::max(from, runs_[irun_].start);
+  }
+
+  // first alive ref with key h visible at p (start order; vis grows with start)
+  int64_t first_alive_ref(uint64_t h, uint64_t p) {
+    auto it = fmap_.find(h);
+    if (it == fmap_.end()) return -1;
+    for (uint32_t ref : it->second) {
+      if (vis_[ref] > p) break;
+      if (!dead_[ref]) return ref;
+    }
+    return -1;
+  }
+
+  void build_fbatch(uint64_t p0) {
+    FBatch b;
+    // predicted positions: p0, p0+1..p0+7 (in case p0 fails), then the
+    // success chain p0+W, p0+2W, ... all restricted to screen runs
+    size_t save = irun_;
+    std::vector<uint64_t> pos;
+    uint64_t q = p0;
+    for (int k = 0; k < 8 && q != kInf; ++k) {
+      q = next_run_pos(q);
+      if (q == kInf) break;
+      pos.push_back(q);
+      ++q;
+    }
+    irun_ = save;
+    q = p0 + W_;
+    while (pos.size() < kFBatchMax) {
+      q = next_run_pos(q);
+      if (q == kInf) break;
+      pos.push_back(q);
+      q += W_;
+    }
+    irun_ = save;
+    std::sort(pos.begin(), pos.end());
+    pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+    const size_t np = pos.size();
+    std::vector<uint64_t> a(np), e(np);
+    for (size_t i = 0; i < np; ++i) {
+      a[i] = pos[i] - W_ + 1;
+      e[i] = pos[i] + 1;
+    }
+    b.h = range_digests(a, e);
+    b.pos = std::move(pos);
+    b.vref.assign(np, -1);
+    b.vok.assign(np, 0);
+    b.has_sha.assign(np, 0);
+    b.sha.assign(np * 20, 0);
+    std::vector<uint64_t> wa, ra;
+    std::vector<size_t> widx;
+    std::vector<uint64_t> sa;
+    std::vector<uint32_t> sl;
+    std::vector<size_t> sidx;
+    for (size_t i = 0; i < np; ++i) {
+      int64_t ref = first_alive_ref(b.h[i], b.pos[i]);
+      if (ref >= 0) {
+        b.vref[i] = ref;
+        wa.push_back(a[i]);
+        ra.push_back(start_[ref]);
+        widx.push_back(i);
+      }
+      if (smap_.count(b.h[i])) {
+        sa.push_back(a[i]);
+        sl.push_back(W_);
+        sidx.push_back(i);
+      }
+    }
+    std::vector<uint8_t> ok = verify_pairs(wa, ra, W_);
+    for (size_t j = 0; j < widx.size(); ++j) b.vok[widx[j]] = ok[j];
+    std::vector<uint8_t> sh = sha1s(sa, sl);
+    for (size_t j = 0; j < sidx.size(); ++j) {
+      b.has_sha[sidx[j]] = 1;
+      memcpy(&b.sha[sidx[j] * 20], &sh[j * 20], 20);
+    }
+    fb_ = std::move(b);
+  }
+
+  // Is p an F match?  Returns the matched key via *key.
+  bool eval_f(uint64_t p, uint64_t* key) {
+    while (fb_.cur < fb_.pos.size() && fb_.pos[fb_.cur] < p) ++fb_.cur;
+    if (fb_.cur == fb_.pos.size() || fb_.pos[fb_.cur] != p) build_fbatch(p);
+    const size_t i = fb_.cur;
+    const uint64_t h = fb_.h[i];
+    *key = h;
+    // in-stream anchorless chunks: content equality with an alive visible ref
+    auto it = fmap_.find(h);
+    if (it != fmap_.end()) {
+      for (uint32_t ref : it->second) {
+        if (vis_[ref] > p) break;
+        if (dead_[ref]) continue;
+        bool ok;
+        if (fb_.vref[i] == (int64_t)ref) {
+          ok = fb_.vok[i];
+        } else {
+          std::vector<uint64_t> wa{p - W_ + 1}, ra{start_[ref]};
+          ok = verify_pairs(wa, ra, W_)[0];
+        }
+        if (ok) return true;
+      }
+    }
+    // static index entries: SHA-1 prefix of the window (chunk_index.cc:130-139)
+    auto st = smap_.find(h);
+    if (st != smap_.end()) {
+      if (!fb_.has_sha[i]) {
+        std::vector<uint64_t> sa{p - W_ + 1};
+        std::vector<uint32_t> sl{W_};
+        std::vector<uint8_t> sh = sha1s(sa, sl);
+        memcpy(&fb_.sha[i * 20], sh.data(), 20);
+        fb_.has_sha[i] = 1;
+      }
+      for (uint32_t si : st->second)
+        if (memcmp(c_.statics[si].sha, &fb_.sha[i * 20], 16) == 0) return true;
+    }
+    return false;
+  }
+
+  uint64_t next_f(uint64_t x, uint64_t limit, uint64_t* key) {
+    if (!has_f_) return kInf;
+    uint64_t p = std::max(x, f_min_vis_);
+    for (;;) {
+      p = next_run_pos(p);
+      if (p == kInf || p >= limit) return kInf;
+      if (eval_f(p, key)) return p;
+      ++p;
+    }
+  }
+
+  // ---------------------------------------------------------------- walk
+  bool alive_visible(uint32_t ref, uint64_t p) const { return vis_[ref] <= p && !dead_[ref]; }
+
+  void push(uint64_t off, uint32_t size, uint32_t kind, uint64_t rolling) {
+    zc_record r;
+    memset(&r, 0, sizeof r);
+    r.offset = off;
+    r.size = size;
+    r.kind = kind;
+    r.rolling = rolling;
+    c_.recs.push_back(r);
+  }
+
+  // a cut piece [a, b) saved via saveChunkToSave (digest filled in later)
+  void piece(uint64_t a, uint64_t b) {
+    const uint32_t len = (uint32_t)(b - a);
+    if (len < 128) {
+      push(a, len, ZC_BYTES, 0);
+    } else {
+      need_digest_.push_back({c_.recs.size(), a, b});
+      push(a, len, ZC_CHUNK_NEW, 0);
+    }
+  }
+
+  // save the grid chunks of this epoch whose cut happens at or before probe m
+  void save_grid_until(uint64_t m) {
+    while (ks_ < nspec_) {
+      const uint64_t ck = r_e_ + ks_ * W_;
+      if (ck + 2ull * W_ - 1 > m) break;
+      const bool dead = indexable_ && dead_[nconf_ + ks_];
+      if (!dead && ck >= s_) {
+        if (indexable_) {
+          push(ck, W_, ZC_CHUNK_NEW, key_[nconf_ + ks_]);
+        } else {
+          push(ck, W_, ZC_BYTES, 0);
+        }
+        s_ = ck + W_;
+      }
+      ++ks_;
+    }
+  }
+
+  void finish() {
+    save_grid_until(kInf);
+    const uint64_t L = n_ - s_;
+    if (L > W_) {
+      piece(s_, s_ + W_);
+      piece(s_ + W_, n_);
+    } else if (L > 0) {
+      piece(s_, n_);
+    }
+    s_ = n_;
+  }
+
+  bool walk() {
+    uint64_t x = r_ + W_ - 1;
+    size_t ia = 0;
+    irun_ = 0;
+    for (;;) {
+      if (x >= n_) {
+        finish();
+        return false;
+      }
+      uint64_t pa = kInf;
+      uint32_t refa = 0;
+      while (ia < acands_.size()) {
+        const ACand& a = acands_[ia];
+        if (a.p >= x && alive_visible(a.ref, a.p)) {
+          pa = a.p;
+          refa = a.ref;
+          break;
+        }
+        ++ia;
+      }
+      uint64_t fkey = 0;
+      uint64_t pf = next_f(x, pa == kInf ? kInf : pa + 1, &fkey);
+      if (pa == kInf && pf == kInf) {
+        finish();
+        return false;
+      }
+      uint64_t m, key;
+      if (pf != kInf && (pa == kInf || pf < pa)) {
+        m = pf;
+        key = fkey;
+      } else {
+        m = pa;
+        key = key_[refa];
+      }
+      // the match at m
+      save_grid_until(m);
+      const uint64_t ws = m - W_ + 1;
+      if (ws > s_) piece(s_, ws);
+      push(ws, W_, ZC_CHUNK_DUP, key);
+      r_ = m + 1;
+      s_ = r_;
+      if ((r_ - r_e_) % W_ == 0) {
+        // same grid: the grid chunk the window covered is consumed, not saved
+        const uint64_t j = (ws - r_e_) / W_;
+        if (indexable_ && j < nspec_) dead_[nconf_ + j] = 1;
+        if (j >= ks_) ks_ = j + 1;
+        x = r_ + W_ - 1;
+        continue;
+      }
+      // grid shift: keep the saved chunks of this epoch, start a new one
+      std::vector<uint32_t> keep;
+      for (uint32_t k = 0; k < (indexable_ ? nspec_ : 0); ++k) {
+        uint32_t ref = nconf_ + k;
+        if (!dead_[ref] && vis_[ref] <= m) keep.push_back(ref);
+      }
+      for (uint32_t ref : keep) {
+        start_[nconf_] = start_[ref];
+        key_[nconf_] = key_[ref];
+        fp_[nconf_] = fp_[ref];
+        anc_[nconf_] = anc_[ref];
+        vis_[nconf_] = 0;  // saved before r: visible to every later probe
+        ++nconf_;
+      }
+      return true;
+    }
+  }
+
+  // ---------------------------------------------------------------- finalize
+  void finalize() {
+    std::vector<uint64_t> a, b;
+    for (auto& pc : need_digest_) {
+      a.push_back(pc.a);
+      b.push_back(pc.b);
+    }
+    std::vector<uint64_t> h = range_digests(a, b);
+    for (size_t i = 0; i < need_digest_.size(); ++i) c_.recs[need_digest_[i].rec].rolling = h[i];
+    if (c_.flags & ZC_FLAG_SHA1) {
+      std::vector<uint64_t> sa;
+      std::vector<uint32_t> sl;
+      std::vector<size_t> idx;
+      for (size_t i = 0; i < c_.recs.size(); ++i)
+        if (c_.recs[i].kind != ZC_BYTES) {
+          sa.push_back(c_.recs[i].offset);
+          sl.push_back(c_.recs[i].size);
+          idx.push_back(i);
+        }
+      for (size_t off = 0; off < sa.size(); off += kFBatchMax) {
+        size_t m = std::min(sa.size() - off, kFBatchMax);
+        std::vector<uint64_t> pa(sa.begin() + off, sa.begin() + off + m);
+        std::vector<uint32_t> pl(sl.begin() + off, sl.begin() + off + m);
+        std::vector<uint8_t> sh = sha1s(pa, pl);
+        for (size_t j = 0; j < m; ++j) memcpy(c_.recs[idx[off + j]].sha1, &sh[j * 20], 16);
+      }
+      // Writer::add -> ChunkIndex::addChunk: later streams on this context
+      // can match this stream's new chunks (only W-byte chunks can match)
+      for (const zc_record& r : c_.recs)
+        if (r.kind == ZC_CHUNK_NEW && r.size == W_) {
+          StaticEntry e;
+          e.key = r.rolling;
+          memcpy(e.sha, r.sha1, 16);
+          c_.statics.push_back(e);
+        }
+    }
+  }
+};
+
+int fail(zc_ctx* c, const ZcError& e) {
+  if (c) c->err = e.msg;
+  return e.code;
+}
+
+template <class F>
+int guarded(zc_ctx* c, F&& f) {
+  try {
+    f();
+    if (c) c->err.clear();
+    return ZC_OK;
+  } catch (const ZcError& e) {
+    return fail(c, e);
+  } catch (const std::bad_alloc&) {
+    return fail(c, ZcError{ZC_ERR_NOMEM, "host allocation failed"});
+  } catch (const std::exception& e) {
+    return fail(c, ZcError{ZC_ERR_STATE, e.what()});
+  }
+}
+
+void append_device(zc_ctx& c, const void* src, size_t n, hipMemcpyKind kind) {
+  if (!n) return;
+  if (c.n_stream + n > c.d_stream.cap) {
+    size_t want = std::max<size_t>(c.n_stream + n, c.d_stream.cap * 2);
+    want = (want + 4095) & ~size_t(4095);
+    uint8_t* np = nullptr;
+    hipError_t e = hipMalloc(&np, want);
+    if (e != hipSuccess) throw ZcError{ZC_ERR_NOMEM, std::string("stream buffer: ") + hipGetErrorString(e)};
+    if (c.n_stream)
+      HCK(hipMemcpyAsync(np, c.d_stream.p, c.n_stream, hipMemcpyDeviceToDevice, c.stream));
+    sync(c);
+    c.d_stream.release();
+    c.d_stream.p = np;
+    c.d_stream.cap = want;
+  }
+  HCK(hipMemcpyAsync(c.d_stream.p + c.n_stream, src, n, kind, c.stream));
+  sync(c);
+  c.n_stream += n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zc_abi_version(void) { return ZCHUNK_ABI_VERSION; }
+
+int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags) {
+  if (!out || chunk_max_size == 0) return ZC_ERR_ARG;
+  *out = nullptr;
+  zc_ctx* c = new (std::nothrow) zc_ctx;
+  if (!c) return ZC_ERR_NOMEM;
+  c->device = device;
+  c->W = chunk_max_size;
+  c->flags = flags;
+  int rc = guarded(c, [&] {
+    DeviceGuard g(device);
+    HCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HCK(hipEventCreate(&c->ev0));
+    HCK(hipEventCreate(&c->ev1));
+    HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
+  });
+  if (rc != ZC_OK) {
+    zc_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return ZC_OK;
+}
+
+int zc_destroy(zc_ctx* c) {
+  if (!c) return ZC_ERR_ARG;
+  {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stage) (void)hipHostFree(c->stage);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  return ZC_OK;
+}
+
+int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
+  if (!c || (n && !seeds)) return ZC_ERR_ARG;
+  return guarded(c, [&] {
+    for (size_t i = 0; i < n; ++i) {
+      if (seeds[i].size != c->W) continue;  // only W-byte entries can equal a W-byte window
+      StaticEntry e;
+      e.key = seeds[i].rolling;
+      memcpy(e.sha, seeds[i].sha1, 16);
+      c->statics.push_back(e);
+    }
+  });
+}
+
+void* zc_get_input_buffer(zc_ctx* c) { return (c && !c->finished) ? c->stage : nullptr; }
+
+size_t zc_get_input_buffer_size(zc_ctx* c) { return (c && !c->finished) ? kFeedChunk : 0; }
+
+int zc_handle_more_data(zc_ctx* c, size_t added) {
+  if (!c || added > kFeedChunk) return ZC_ERR_ARG;
+  if (c->finished) return ZC_ERR_STATE;
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    append_device(*c, c->stage, added, hipMemcpyHostToDevice);
+  });
+}
+
+int zc_feed(zc_ctx* c, const void* host, size_t n) {
+  if (!c || (n && !host)) return ZC_ERR_ARG;
+  if (c->finished) return ZC_ERR_STATE;
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    append_device(*c, host, n, hipMemcpyHostToDevice);
+  });
+}
+
+int zc_finish(zc_ctx* c) {
+  if (!c) return ZC_ERR_ARG;
+  if (c->finished) return ZC_ERR_STATE;
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    Resolver res(*c, c->d_stream.p, c->n_stream);
+    res.run();
+    c->d_last = c->d_stream.p;
+    c->n_last = c->n_stream;
+    c->finished = true;
+  });
+}
+
+int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
+  if (!c || (n && !d_data) || ((uintptr_t)d_data & 15)) return ZC_ERR_ARG;
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    Resolver res(*c, (const uint8_t*)d_data, n);
+    res.run();
+    c->d_last = (const uint8_t*)d_data;
+    c->n_last = n;
+    c->finished = true;
+  });
+}
+
+size_t zc_record_count(const zc_ctx* c) { return c ? c->recs.size() : 0; }
+
+int zc_get_records(const zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
+  if (!c || (cap && !out)) return ZC_ERR_ARG;
+  size_t n = std::min(cap, c->recs.size());
+  if (n) memcpy(out, c->recs.data(), n * sizeof(zc_record));
+  if (n_out) *n_out = n;
+  return ZC_OK;
+}
+
+int zc_get_stats(const zc_ctx* c, zc_stats* out) {
+  if (!c || !out) return ZC_ERR_ARG;
+  *out = c->stats;
+  return ZC_OK;
+}
+
+int zc_reset(zc_ctx* c) {
+  if (!c) return ZC_ERR_ARG;
+  c->n_stream = 0;
+  c->finished = false;
+  c->d_last = nullptr;
+  c->n_last = 0;
+  c->recs.clear();
+  c->err.clear();
+  return ZC_OK;
+}
+
+int zc_read_stream(const zc_ctx* c, uint64_t offset, size_t n, void* host_out) {
+  if (!c || (n && !host_out) || offset > c->n_last || n > c->n_last - offset) return ZC_ERR_ARG;
+  if (!n) return ZC_OK;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(c->device) != hipSuccess) return ZC_ERR_HIP;
+  hipError_t e = hipMemcpy(host_out, c->d_last + offset, n, hipMemcpyDeviceToHost);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return e == hipSuccess ? ZC_OK : ZC_ERR_HIP;
+}
+
+const char* zc_last_error(const zc_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int zc_fill_splitmix64(void* d_data, uint64_t n, uint64_t seed, int device) {
+  if (n && !d_data) return ZC_ERR_ARG;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return ZC_ERR_HIP;
+  hipError_t e = launch_fill_splitmix64((uint8_t*)d_data, n, seed, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return e == hipSuccess ? ZC_OK : ZC_ERR_HIP;
+}
+
+}  // extern "C"
