@@ -1,0 +1,51 @@
+// Ablation timing of zc_scan_kernel variants (ablation bits in zc_kernels.hip),
+// interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
+// Tooling only.  Build: hipcc -O3 --offload-arch=gfx950 -I../../zbackup_amd/csrc scan_ablate.hip
+#include "../../zbackup_amd/csrc/zc_kernels.hip"
+
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+
+using namespace zc;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+int main(int argc, char** argv) {
+  uint64_t n = argc > 1 ? strtoull(argv[1], 0, 0) : (8ull << 30);
+  uint8_t* d; CK(hipMalloc(&d, n));
+  CK(launch_fill_splitmix64(d, n, 2024, 0));
+  uint64_t ntiles = n / ZC_STILE, nslots = ntiles * ZC_SCAN_TPB;
+  int cus = cu_count();
+  uint64_t* blk; uint16_t* arel; uint32_t* afp; uint32_t* acnt; uint32_t* ovf; unsigned long long* cnt;
+  CK(hipMalloc(&blk, n / ZC_SPAN * 8)); CK(hipMalloc(&arel, nslots * ZC_ANC_SLOTS * 2));
+  CK(hipMalloc(&afp, nslots * ZC_ANC_SLOTS * 4)); CK(hipMalloc(&acnt, nslots * 4));
+  CK(hipMalloc(&ovf, 1 << 20)); CK(hipMalloc(&cnt, 64));
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, int32_t, uint64_t*, uint16_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t, unsigned long long*); std::vector<float> t; };
+  std::vector<V> vs = {
+    {"full", zc_scan_kernel<0>, {}},
+    {"no_record", zc_scan_kernel<ABL_NO_RECORD>, {}},
+    {"no_digest", zc_scan_kernel<ABL_NO_DIGEST>, {}},
+    {"no_digest_no_record", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_RECORD>, {}},
+    {"digest_only", zc_scan_kernel<ABL_NO_GEAR>, {}},
+    {"stage_only", zc_scan_kernel<ABL_NO_BYTES>, {}},
+    {"gear_digest_nobranch", zc_scan_kernel<ABL_NO_BRANCH>, {}},
+    {"gear_nobranch", zc_scan_kernel<ABL_NO_BRANCH | ABL_NO_DIGEST>, {}},
+    {"full_never_taken", zc_scan_kernel<ABL_NEVER>, {}},
+    {"gear_never_taken", zc_scan_kernel<ABL_NEVER | ABL_NO_DIGEST>, {}},
+  };
+  for (int round = 0; round < 6; ++round)
+    for (auto& v : vs) {
+      CK(hipMemset(cnt, 0, 64));
+      CK(hipEventRecord(a));
+      hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, ntiles, anchor_lo_for(65536), blk, arel, afp, acnt, ovf, 1u << 16, cnt);
+      CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+      float ms; CK(hipEventElapsedTime(&ms, a, b));
+      if (round) v.t.push_back(ms);
+    }
+  for (auto& v : vs) {
+    std::sort(v.t.begin(), v.t.end());
+    printf("%-22s median %7.3f ms  min %7.3f ms  %7.1f GB/s\n", v.name, v.t[v.t.size() / 2], v.t[0], n / (v.t[0] * 1e6));
+  }
+  return 0;
+}

@@ -11,26 +11,48 @@ namespace zc {
 // Stream geometry.  One lane owns a contiguous span of ZC_SPAN bytes; the
 // 64-bit Rabin-Karp digest of every span is kept (the "block digests"), so
 // the rolling hash of any byte range is a short Horner fold over spans.
-constexpr int ZC_SPAN = 1024;
+constexpr int ZC_SPAN = 1024;                                // digest granularity
 constexpr int ZC_TPB = 256;                                  // 4 waves
-constexpr uint64_t ZC_TILE = (uint64_t)ZC_SPAN * ZC_TPB;     // 256 KiB per workgroup
-constexpr int ZC_LANE_SLOTS = 8;                             // LDS anchor slots per lane
+// zc_scan: 512-lane persistent workgroups, lane span 4 KiB (2 MiB tiles),
+// per-wave LDS rings of ZC_RING slots of 128-byte rounds
+constexpr int ZC_SCAN_TPB = 512;
+constexpr int ZC_LSPAN = 4096;
+constexpr uint64_t ZC_STILE = (uint64_t)ZC_LSPAN * ZC_SCAN_TPB;
+constexpr int ZC_ROUND = 128;
+constexpr int ZC_RING = 2;
+constexpr int ZC_WLIST = 320;                                // per-wave LDS anchor list entries
+constexpr int ZC_ANC_SLOTS = 16;                             // anchor slots per lane span
+// zc_fscan: lane span 1 KiB, 256 KiB per workgroup
+constexpr uint64_t ZC_TILE = (uint64_t)ZC_SPAN * ZC_TPB;
 constexpr int ZC_RUN_SLOTS = 4;                              // LDS screen-run slots per lane
 
 // Content anchors.  gear(q) = sum_{j<32} b[q-j] * 2^j (mod 2^32); q is an
-// anchor iff (int32)gear(q) >= ZC_ANCHOR_LO, i.e. gear in [0x7FC00000,
-// 0x7FFFFFFF] (1 position in 1024 for random bytes; never inside a run of
-// one repeated byte, whose gear is 0 or -c).  The anchor fingerprint is
-// (hist(q) << 32) | gear(q) where hist collects bit 31 of the 32 previous
-// gear values; it depends on the 63 bytes ending at q, so a chunk's anchor
-// offset must be >= ZC_ANCHOR_MIN_OFF.
-constexpr int32_t ZC_ANCHOR_LO = 0x7FC00000;
+// anchor iff (int32)gear(q) >= anchor_lo, i.e. gear in [anchor_lo, 0x7FFFFFFF]:
+// 1 position in rate_inv for random bytes (rate_inv = 2^32 / (2^31 - anchor_lo),
+// chosen per stream from W so a W-byte chunk holds ~16 anchors), never inside a
+// run of one repeated byte (gear 0 or -c).  A chunk's anchor is its first one
+// at offset >= ZC_ANCHOR_MIN_OFF; the table key is the gear value, confirmed
+// by a 64-bit fingerprint of the 64 bytes ending at the anchor.
 constexpr uint32_t ZC_ANCHOR_MIN_OFF = 63;
 constexpr uint32_t ZC_NO_ANCHOR = 0xFFFFFFFFu;
 
-struct Anchor {
-  uint64_t pos;
-  uint64_t fp;
+inline int32_t anchor_lo_for(uint32_t W) {
+  uint32_t rate_inv = 16;
+  while (rate_inv < 4096 && rate_inv * 2 <= W / 16) rate_inv *= 2;
+  return (int32_t)(0x80000000u - (uint32_t)(0x100000000ull / rate_inv));
+}
+
+// Anchors of the stream, per 4 KiB lane span s: cnt[s] anchors, in position
+// order; if cnt[s] <= ZC_ANC_SLOTS they sit in the fixed slots
+// rel/g[s * ZC_ANC_SLOTS ...], otherwise in the overflow pool at ovf_off[s].
+// Position = s * ZC_LSPAN + rel; g = gear value at that position.
+struct AnchorView {
+  const uint32_t* cnt;
+  const uint16_t* rel;
+  const uint32_t* g;
+  const uint64_t* ovf_off;
+  const uint16_t* orel;
+  const uint32_t* og;
 };
 
 struct Run {  // maximal run [start, end) of screen hits of the F scan
@@ -44,26 +66,33 @@ struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
 };
 
 // Counters word layout (uint64 each)
-enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_LAST = 8 };
+// CNT_POOL: anchors found; CNT_OVERFLOW: lane spans over ZC_ANC_SLOTS anchors;
+// CNT_FOVF: screen-run buffer overflow flag
+enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_LAST = 8 };
 
 // --- launchers (return hipError_t of the launch) ---------------------------
-hipError_t launch_scan(const uint8_t* data, uint64_t n, uint64_t* blk, Anchor* pool,
-                       uint64_t pool_cap, uint64_t* tile_off, uint32_t* tile_cnt,
+hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, uint16_t* arel,
+                       uint32_t* ag, uint32_t* acnt, uint32_t* ovf_list, uint32_t ovf_cap,
                        unsigned long long* counters, hipStream_t s);
 
-hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk,
-                             const Anchor* pool, const uint64_t* tile_off, const uint32_t* tile_cnt,
+// ovf_list holds (span, count) pairs of lane spans with more than
+// ZC_ANC_SLOTS anchors; the dense kernel writes ovf_off[span] = offs[i] and
+// the span's anchors at that offset of the overflow pool
+hipError_t launch_anchor_dense(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* spans,
+                               uint32_t nspans, const uint64_t* offs, uint64_t* ovf_off, uint16_t* orel,
+                               uint32_t* og, hipStream_t s);
+
+hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av,
                              const uint64_t* starts, uint32_t nchunks, uint32_t W, uint64_t pw,
-                             uint64_t* key, uint64_t* fp, uint32_t* anc_off, hipStream_t s);
+                             uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off, hipStream_t s);
 
 hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s);
 hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,
-                               const uint64_t* fp, const uint32_t* anc_off, uint32_t nrefs,
+                               const uint32_t* cg, const uint32_t* anc_off, uint32_t nrefs,
                                hipStream_t s);
 
-hipError_t launch_probe(const Anchor* pool, uint64_t npool, const uint64_t* tkeys,
-                        const uint32_t* tvals, uint32_t tbits, const uint64_t* chunk_start,
-                        const uint32_t* anc_off, const uint64_t* vis, const uint8_t* dead,
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nspans, const uint64_t* tkeys,
+                        const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp, const uint64_t* vis, const uint8_t* dead,
                         uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
                         unsigned long long* counters, hipStream_t s);
 

@@ -110,12 +110,15 @@ struct zc_ctx {
   zc_stats stats{};
 
   // scratch
-  DevBuf<uint64_t> blk, tile_off, ftile_off;
-  DevBuf<uint32_t> tile_cnt, ftile_cnt;
-  DevBuf<Anchor> pool;
+  DevBuf<uint64_t> blk, ftile_off;
+  DevBuf<uint32_t> ftile_cnt;
+  DevBuf<uint16_t> arel, orel;
+  DevBuf<uint32_t> ag, og;
+  DevBuf<uint64_t> ovf_off;
+  DevBuf<uint32_t> acnt, ovf_list;
   DevBuf<unsigned long long> counters;
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
-  DevBuf<uint32_t> c_anc;
+  DevBuf<uint32_t> c_anc, c_g;
   DevBuf<uint8_t> c_dead;
   DevBuf<uint64_t> tkeys;
   DevBuf<uint32_t> tvals;
@@ -183,14 +186,17 @@ class Resolver {
   const uint32_t W_;
   const bool indexable_;
   uint64_t npool_ = 0;
+  uint64_t nls_ = 0;  // lane spans of the stream
+  const int32_t anchor_lo_ = anchor_lo_for(W_);
+  AnchorView av_{};
 
   // resolver state
   uint64_t r_ = 0, s_ = 0, r_e_ = 0;
 
   // refs = indexable W-byte chunks that can be matched: [0, nconf_) saved in
   // earlier epochs, [nconf_, nconf_+nspec_) this epoch's grid chunks
-  std::vector<uint64_t> start_, key_, fp_, vis_;
-  std::vector<uint32_t> anc_;
+  std::vector<uint64_t> start_, key_, fp_, vis_;  // fp_: 64-byte anchor fingerprint
+  std::vector<uint32_t> anc_, g_;                  // g_: anchor gear value
   std::vector<uint8_t> dead_;
   uint32_t nconf_ = 0, nspec_ = 0;
   uint64_t ks_ = 0;  // next grid chunk of this epoch to save
@@ -225,36 +231,75 @@ class Resolver {
 
   // ---------------------------------------------------------------- scan
   void scan() {
-    const uint64_t ntiles = (n_ + ZC_TILE - 1) / ZC_TILE;
-    const uint64_t nspans = (n_ + ZC_SPAN - 1) / ZC_SPAN;
-    c_.blk.ensure(nspans);
-    c_.tile_off.ensure(ntiles);
-    c_.tile_cnt.ensure(ntiles);
+    const uint64_t ntiles = (n_ + ZC_STILE - 1) / ZC_STILE;
+    const uint64_t nslots = ntiles * ZC_SCAN_TPB;  // lane spans, incl. ones past the end
+    nls_ = (n_ + ZC_LSPAN - 1) / ZC_LSPAN;
+    const uint32_t ovf_cap = 1u << 16;
+    c_.blk.ensure((n_ + ZC_SPAN - 1) / ZC_SPAN);
+    c_.acnt.ensure(nslots);
+    c_.arel.ensure(nslots * ZC_ANC_SLOTS);
+    c_.ag.ensure(nslots * ZC_ANC_SLOTS);
+    c_.ovf_list.ensure(2 * ovf_cap);
     c_.counters.ensure(CNT_LAST);
-    uint64_t cap = std::max<uint64_t>(n_ / 512, 4096);
-    for (int attempt = 0; attempt < 3; ++attempt) {
-      c_.pool.ensure(cap);
-      HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
-      if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
-      HCK(launch_scan(d_, n_, c_.blk.p, c_.pool.p, c_.pool.cap, c_.tile_off.p, c_.tile_cnt.p,
-                      c_.counters.p, c_.stream));
-      if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
-      unsigned long long cnt[CNT_LAST];
-      d2h(c_, cnt, c_.counters.p, CNT_LAST);
-      sync(c_);
-      if (c_.flags & ZC_FLAG_TIMING) {
-        float ms = 0;
-        HCK(hipEventElapsedTime(&ms, c_.ev0, c_.ev1));
-        c_.stats.scan_ms = ms;
-      }
-      if (!(cnt[CNT_OVERFLOW] & 1)) {
-        npool_ = cnt[CNT_POOL];
-        c_.stats.anchors = npool_;
-        return;
-      }
-      cap = cnt[CNT_POOL] + cnt[CNT_POOL] / 8 + 4096;
+    HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+    if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
+    HCK(launch_scan(d_, n_, anchor_lo_, c_.blk.p, c_.arel.p, c_.ag.p, c_.acnt.p, c_.ovf_list.p, ovf_cap,
+                    c_.counters.p, c_.stream));
+    if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
+    unsigned long long cnt[CNT_LAST];
+    d2h(c_, cnt, c_.counters.p, CNT_LAST);
+    sync(c_);
+    if (c_.flags & ZC_FLAG_TIMING) {
+      float ms = 0;
+      HCK(hipEventElapsedTime(&ms, c_.ev0, c_.ev1));
+      c_.stats.scan_ms = ms;
     }
-    throw ZcError{ZC_ERR_NOMEM, "anchor pool overflow persisted"};
+    npool_ = cnt[CNT_POOL];
+    c_.stats.anchors = npool_;
+    const uint64_t novf = cnt[CNT_OVERFLOW];
+    c_.ovf_off.ensure(novf ? nls_ : 1);
+    if (novf) {
+      // lane spans with more anchors than slots: rescan them into an exactly
+      // sized overflow pool.  The scan listed them as (span, count) pairs.
+      std::vector<uint32_t> spans, counts;
+      if (novf <= ovf_cap) {
+        std::vector<uint32_t> pairs(2 * novf);
+        d2h(c_, pairs.data(), c_.ovf_list.p, 2 * novf);
+        sync(c_);
+        for (uint64_t k = 0; k < novf; ++k) {
+          spans.push_back(pairs[2 * k]);
+          counts.push_back(pairs[2 * k + 1]);
+        }
+      } else {  // list overflowed too (very dense data): read all counts
+        std::vector<uint32_t> all(nls_);
+        d2h(c_, all.data(), c_.acnt.p, nls_);
+        sync(c_);
+        for (uint64_t sx = 0; sx < nls_; ++sx)
+          if (all[sx] > ZC_ANC_SLOTS) {
+            spans.push_back((uint32_t)sx);
+            counts.push_back(all[sx]);
+          }
+      }
+      std::vector<uint64_t> offs(spans.size());
+      uint64_t total = 0;
+      for (size_t k = 0; k < spans.size(); ++k) {
+        offs[k] = total;
+        total += counts[k];
+      }
+      c_.orel.ensure(total);
+      c_.og.ensure(total);
+      c_.ovf_list.ensure(std::max<size_t>(spans.size(), 2 * ovf_cap));
+      c_.va.ensure(spans.size());
+      h2d(c_, c_.ovf_list.p, spans.data(), spans.size());
+      h2d(c_, c_.va.p, offs.data(), offs.size());
+      HCK(launch_anchor_dense(d_, n_, anchor_lo_, c_.ovf_list.p, (uint32_t)spans.size(), c_.va.p,
+                              c_.ovf_off.p, c_.orel.p, c_.og.p, c_.stream));
+      sync(c_);
+    } else {
+      c_.orel.ensure(1);
+      c_.og.ensure(1);
+    }
+    av_ = AnchorView{c_.acnt.p, c_.arel.p, c_.ag.p, c_.ovf_off.p, c_.orel.p, c_.og.p};
   }
 
   // ---------------------------------------------------------------- epoch
@@ -269,6 +314,7 @@ class Resolver {
     start_.resize(nref);
     key_.resize(nref);
     fp_.resize(nref);
+    g_.resize(nref);
     vis_.resize(nref);
     anc_.resize(nref);
     dead_.assign(nref, 0);
@@ -288,19 +334,22 @@ class Resolver {
       c_.c_fp.ensure(nref);
       c_.c_vis.ensure(nref);
       c_.c_anc.ensure(nref);
+      c_.c_g.ensure(nref);
       c_.c_dead.ensure(nref);
       h2d(c_, c_.c_start.p, start_.data(), nref);
       h2d(c_, c_.c_key.p, key_.data(), nconf_);
       h2d(c_, c_.c_fp.p, fp_.data(), nconf_);
       h2d(c_, c_.c_anc.p, anc_.data(), nconf_);
+      h2d(c_, c_.c_g.p, g_.data(), nconf_);
       h2d(c_, c_.c_vis.p, vis_.data(), nref);
       h2d(c_, c_.c_dead.p, dead_.data(), nref);
-      HCK(launch_chunk_meta(d_, n_, c_.blk.p, c_.pool.p, c_.tile_off.p, c_.tile_cnt.p,
-                            c_.c_start.p + nconf_, nrefs_spec, W_, pow257(W_), c_.c_key.p + nconf_,
+      HCK(launch_chunk_meta(d_, n_, c_.blk.p, av_, c_.c_start.p + nconf_,
+                            nrefs_spec, W_, pow257(W_), c_.c_key.p + nconf_, c_.c_g.p + nconf_,
                             c_.c_fp.p + nconf_, c_.c_anc.p + nconf_, c_.stream));
       d2h(c_, key_.data() + nconf_, c_.c_key.p + nconf_, nrefs_spec);
       d2h(c_, fp_.data() + nconf_, c_.c_fp.p + nconf_, nrefs_spec);
       d2h(c_, anc_.data() + nconf_, c_.c_anc.p + nconf_, nrefs_spec);
+      d2h(c_, g_.data() + nconf_, c_.c_g.p + nconf_, nrefs_spec);
       sync(c_);
       probe_anchors(nref);
     }
@@ -325,14 +374,13 @@ class Resolver {
     c_.tkeys.ensure(tsize);
     c_.tvals.ensure(tsize);
     HCK(launch_table_clear(c_.tkeys.p, tsize, c_.stream));
-    HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_fp.p, c_.c_anc.p, nref, c_.stream));
+    HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_g.p, c_.c_anc.p, nref, c_.stream));
     uint64_t cap = std::max<uint64_t>(1u << 16, nanc);
     unsigned long long cnt[CNT_LAST];
     for (int attempt = 0; attempt < 3; ++attempt) {
       c_.cand.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-      HCK(launch_probe(c_.pool.p, npool_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_start.p, c_.c_anc.p,
-                       c_.c_vis.p, c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p,
+      HCK(launch_probe(d_, av_, nls_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p, c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p,
                        c_.stream));
       d2h(c_, cnt, c_.counters.p, CNT_LAST);
       sync(c_);
@@ -437,7 +485,7 @@ class Resolver {
                        c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
       d2h(c_, cnt, c_.counters.p, CNT_LAST);
       sync(c_);
-      if (!(cnt[CNT_OVERFLOW] & 2)) break;
+      if (!cnt[CNT_FOVF]) break;
       cap = cnt[CNT_RUNS] + 1024;
       if (attempt == 2) throw ZcError{ZC_ERR_NOMEM, "screen-run buffer overflow persisted"};
     }
@@ -708,6 +756,7 @@ class Resolver {
         start_[nconf_] = start_[ref];
         key_[nconf_] = key_[ref];
         fp_[nconf_] = fp_[ref];
+        g_[nconf_] = g_[ref];
         anc_[nconf_] = anc_[ref];
         vis_[nconf_] = 0;  // saved before r: visible to every later probe
         ++nconf_;

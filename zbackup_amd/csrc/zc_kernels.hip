@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "zc_device.h"
 
 namespace zc {
@@ -34,6 +36,7 @@ namespace zc {
 namespace {
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ inline uint64_t pow257_dev(uint64_t e) {
   uint64_t r = 1, b = 257;
@@ -119,230 +122,426 @@ __device__ __forceinline__ uint32_t load4_any(const uint8_t* base, uint64_t addr
 }
 
 // ---------------------------------------------------------------------------
-// zc_scan
+// zc_scan (the HBM-bound pass)
+//
+// Persistent workgroups of 512 lanes (8 waves, one workgroup per CU, two
+// waves per SIMD); each lane owns a 4 KiB span, a tile is 512 spans = 2 MiB.
+// Every wave streams its own 64 rows through a private 2-slot LDS ring of
+// 128-byte rounds with global_load_lds_dwordx4; the round after the current
+// one is always in flight, and the ring continues across the workgroup's
+// tiles.  One DMA instruction fills 8 rows x 128 B (whole cache lines); the
+// LDS image is linear and the global source is swizzled (piece p of row i sits
+// at piece p ^ ((i >> 1) & 7)), so the per-lane ds_read_b128 of a row is
+// bank-conflict free (MI355X_MICROARCH.md §LDS lane groups).  Round -1 of a
+// tile stages the bytes before each span (gear warm-up).  Waves never touch
+// each other's LDS: no barriers.  (tools/ubench/stage_bench.hip measured this
+// staging shape at 5.5 TB/s with no per-byte work.)
+//
+// Anchors are appended to a per-wave LDS list (one ballot per dword on the
+// fast path; a wave-uniform block in the ~22 % of dwords where any lane hits)
+// and moved to the per-span global slots once per tile, so no global store is
+// outstanding while the ring is being waited on.
 struct ScanLane {
-  uint32_t glo, ghi;  // gear hash and its 32-position bit-31 history
-  uint32_t hlo, hhi;  // 64-bit Rabin-Karp accumulator of the span so far
+  uint32_t glo;       // gear hash
+  uint32_t hlo, hhi;  // 64-bit Rabin-Karp accumulator of the current 1 KiB span
 };
 
-__device__ __forceinline__ void gear_step(uint32_t b, ScanLane& s) {
-  s.ghi = __builtin_amdgcn_alignbit(s.ghi, s.glo, 31);  // (ghi << 1) | (glo >> 31)
-  s.glo = (s.glo << 1) + b;
-}
+__device__ __forceinline__ void gear_step(uint32_t b, ScanLane& s) { s.glo = (s.glo << 1) + b; }
 
 __device__ __forceinline__ void digest_step(uint32_t b, ScanLane& s) {
-  // acc*257 + b == ((acc << 8) | b) + acc   (mod 2^64)
-  uint32_t slo = (s.hlo << 8) | b;
-  uint32_t shi = __builtin_amdgcn_alignbit(s.hhi, s.hlo, 24);
-  uint64_t h = (((uint64_t)s.hhi << 32) | s.hlo) + (((uint64_t)shi << 32) | slo);
+  // acc*257 + b  (mod 2^64)
+  uint64_t h = (((uint64_t)s.hhi << 32) | s.hlo) * 257u + b;
   s.hlo = (uint32_t)h;
   s.hhi = (uint32_t)(h >> 32);
 }
 
-struct LaneSlots {
-  uint32_t* rel;
-  uint32_t* glo;
-  uint32_t* ghi;
+// 64-bit fingerprint of the 64 bytes ending at anchor position q (q >= 63).
+// Computed lazily from HBM -- only for chunk first-anchors and for stream
+// anchors whose gear value hits the table -- so the scan keeps no per-byte
+// fingerprint state.  Any fixed function of those bytes works: both sides
+// (chunks and stream windows) use this one.
+__device__ __forceinline__ uint32_t load4_any(const uint8_t* base, uint64_t addr);
+__device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
+  uint64_t h = 0x243F6A8885A308D3ull;
+  const uint64_t a = q - (ZC_ANCHOR_MIN_OFF);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    h ^= load4_any(data, a + 4 * i);
+    h *= kGolden;
+    h ^= h >> 29;
+  }
+  return h;
+}
+
+// Ablation bits (tools/ubench/scan_ablate.hip only; the product uses 0):
+// 1 = no digest, 2 = no gear/anchors, 4 = anchors counted but not recorded,
+// 8 = skip the per-byte work entirely (staging + reads only),
+// 16 = gear + max computed but folded into the state without a ballot/branch,
+// 32 = anchor threshold raised so the recording block is (almost) never taken
+enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
+       ABL_NEVER = 32 };
+
+struct WaveList {   // per-wave LDS anchor list: {lane << 16 | rel, gear}
+  uint32_t* e;
+  uint32_t n;       // wave-uniform count (may exceed capacity: then rescan)
 };
 
-__device__ __forceinline__ void record_anchor(const LaneSlots& sl, uint32_t& cnt, uint64_t span0,
-                                              uint32_t rel, uint32_t g, uint32_t gh) {
-  if (span0 + rel < ZC_ANCHOR_MIN_OFF) return;  // window would reach before the stream
-  if (cnt < ZC_LANE_SLOTS) {
-    sl.rel[cnt * ZC_TPB] = rel;
-    sl.glo[cnt * ZC_TPB] = g;
-    sl.ghi[cnt * ZC_TPB] = gh;
-  }
-  ++cnt;
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-template <bool DIGEST>
-__device__ __forceinline__ void scan_dword(uint32_t x, uint32_t rel, ScanLane& s,
-                                           const LaneSlots& sl, uint32_t& cnt, uint64_t span0) {
-  uint32_t g[4], gh[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t b = (x >> (8 * k)) & 0xFFu;
-    gear_step(b, s);
-    if (DIGEST) digest_step(b, s);
-    g[k] = s.glo;
-    gh[k] = s.ghi;
-  }
-  bool any = ((int32_t)g[0] >= ZC_ANCHOR_LO) | ((int32_t)g[1] >= ZC_ANCHOR_LO) |
-             ((int32_t)g[2] >= ZC_ANCHOR_LO) | ((int32_t)g[3] >= ZC_ANCHOR_LO);
-  if (__builtin_expect(any, 0)) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if ((int32_t)g[k] >= ZC_ANCHOR_LO) record_anchor(sl, cnt, span0, rel + k, g[k], gh[k]);
-  }
+// acc += {lo, hi} as ONE v_lshl_add_u64 (written as a 64-bit add of a bit-cast
+// pair; hipcc splits `acc + ((uint64_t)hi << 32 | lo)` into two adds + moves)
+__device__ __forceinline__ void add64_pair(uint32_t& hlo, uint32_t& hhi, uint32_t lo, uint32_t hi) {
+  const v2u32 a = {hlo, hhi}, t = {lo, hi};
+  const uint64_t r = __builtin_bit_cast(uint64_t, a) + __builtin_bit_cast(uint64_t, t);
+  hlo = (uint32_t)r;
+  hhi = (uint32_t)(r >> 32);
 }
 
-// warm the gear with the 64 bytes before the span (virtual zeros before 0)
-__device__ __forceinline__ void gear_warm(const uint8_t* __restrict__ data, uint64_t span0, ScanLane& s) {
-  if (span0 >= 64) {
-    const uint4* w = (const uint4*)(data + span0 - 64);
+// One dword (4 stream bytes) of the scan.  Gear: position k of the dword is
+// g_k = (g << (k+1)) + sum_{j<=k} b_j 2^(k-j), the byte-weighted sums coming
+// from v_dot4_u32_u8, so the four positions are independent of each other.
+// Digest: acc*257 + b = ((acc << 8) | b) + acc, where (acc << 8) | b is one
+// v_perm_b32 (low word) and one v_alignbit_b32 (high word), then one 64-bit
+// add.  Anchor test: one compare of the dword's max gear and one ballot; the
+// recording block below is wave-uniform (the list count stays scalar) and is
+// entered in ~6 % of dwords at the 1/4096 anchor rate.
+template <int ABL>
+__device__ __forceinline__ void scan_dword(uint32_t x, uint32_t rel, uint32_t lane, int32_t lo_thr,
+                                           ScanLane& s, WaveList& wl) {
+  if (ABL & ABL_NO_BYTES) {
+    s.hlo ^= x;
+    return;
+  }
+  uint32_t g[4];
+  if (!(ABL & ABL_NO_GEAR)) {
+    const uint32_t d[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
+                           __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
+                           __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = (s.glo << (k + 1)) + d[k];
+    s.glo = g[3];
+  }
+  if (!(ABL & ABL_NO_DIGEST)) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      uint4 v = w[k];
-      uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
+      const uint32_t slo = __builtin_amdgcn_perm(s.hlo, x, 0x06050400u | k);
+      const uint32_t shi = __builtin_amdgcn_alignbit(s.hhi, s.hlo, 24);
+      add64_pair(s.hlo, s.hhi, slo, shi);
     }
-  } else {
-    for (uint64_t i = 0; i < span0; ++i) gear_step(data[i], s);
+  }
+  if (ABL & ABL_NO_GEAR) return;
+  const int32_t mx = max(max((int32_t)g[0], (int32_t)g[1]), max((int32_t)g[2], (int32_t)g[3]));
+  if (ABL & ABL_NO_BRANCH) {
+    s.hhi ^= (uint32_t)mx;
+    return;
+  }
+  if (ABL & ABL_NEVER) lo_thr = 0x7FFFFFFF;
+  const uint64_t any = __ballot(mx >= lo_thr);
+  if (__builtin_expect(any != 0, 0)) {
+    if (ABL & ABL_NO_RECORD) {
+      wl.n += __popcll(any);
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t mk = __ballot((int32_t)g[k] >= lo_thr);
+      if (mk) {
+        const uint32_t idx = wl.n + lane_prefix(mk);
+        if (((mk >> lane) & 1) && idx < ZC_WLIST) {
+          uint32_t* e = wl.e + idx * 2;
+          e[0] = (lane << 16) | (rel + k);
+          e[1] = g[k];
+        }
+        wl.n += __popcll(mk);
+      }
+    }
   }
 }
 
-__global__ void __launch_bounds__(ZC_TPB) zc_scan_kernel(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t* __restrict__ blk,
-    Anchor* __restrict__ pool, uint64_t pool_cap, uint64_t* __restrict__ tile_off,
-    uint32_t* __restrict__ tile_cnt, unsigned long long* __restrict__ counters) {
-  __shared__ uint32_t s_rel[ZC_LANE_SLOTS * ZC_TPB];
-  __shared__ uint32_t s_glo[ZC_LANE_SLOTS * ZC_TPB];
-  __shared__ uint32_t s_ghi[ZC_LANE_SLOTS * ZC_TPB];
-  __shared__ uint32_t s_tmp[ZC_TPB / 64];
-  __shared__ uint64_t s_base;
-
-  const uint32_t tid = threadIdx.x;
-  const uint64_t tile = blockIdx.x;
-  const uint64_t span0 = tile * ZC_TILE + (uint64_t)tid * ZC_SPAN;
-  LaneSlots sl{s_rel + tid, s_glo + tid, s_ghi + tid};
+// exact anchors of one span straight from global memory (the stream's partial
+// last tile, and waves whose LDS list overflowed): slots, count, overflow pair
+__device__ void span_anchors_rescan(const uint8_t* __restrict__ data, uint64_t n, uint64_t span0,
+                                    int32_t lo_thr, bool digest, uint64_t* __restrict__ blk,
+                                    uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
+                                    uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list,
+                                    uint32_t ovf_cap, unsigned long long* __restrict__ counters) {
+  const uint64_t sidx = span0 / ZC_LSPAN;
+  ScanLane s{0, 0, 0};
+  if (span0 >= 64) {
+    for (uint64_t i = span0 - 64; i < span0; ++i) gear_step(data[i], s);
+  }
+  const uint64_t end = (span0 + ZC_LSPAN < n) ? span0 + ZC_LSPAN : n;
   uint32_t cnt = 0;
+  for (uint64_t p = span0; p < end; ++p) {
+    uint32_t b = data[p];
+    gear_step(b, s);
+    if (digest) {
+      digest_step(b, s);
+      if ((p + 1) % ZC_SPAN == 0 || p + 1 == end) {
+        blk[p / ZC_SPAN] = ((uint64_t)s.hhi << 32) | s.hlo;
+        s.hlo = s.hhi = 0;
+      }
+    }
+    if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) {
+      if (cnt < ZC_ANC_SLOTS) {
+        arel[sidx * ZC_ANC_SLOTS + cnt] = (uint16_t)(p - span0);
+        ag[sidx * ZC_ANC_SLOTS + cnt] = s.glo;
+      }
+      ++cnt;
+    }
+  }
+  acnt[sidx] = cnt;
+  if (cnt > ZC_ANC_SLOTS) {
+    unsigned long long k = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+    if (k < ovf_cap) {
+      ovf_list[2 * k] = (uint32_t)sidx;
+      ovf_list[2 * k + 1] = cnt;
+    }
+  }
+  if (cnt) atomicAdd(&counters[CNT_POOL], (unsigned long long)cnt);
+}
 
-  if (span0 < n) {
-    ScanLane s{0, 0, 0, 0};
-    gear_warm(data, span0, s);
-    const uint64_t len = (n - span0 < ZC_SPAN) ? (n - span0) : ZC_SPAN;
-    if (len == ZC_SPAN) {
-      const uint4* p = (const uint4*)(data + span0);
-      uint4 cur[8], nxt[8];
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int kRoundsPerTile = ZC_LSPAN / ZC_ROUND + 1;  // + warm-up round
+
+// DMA of virtual round R (tile k = R / kRoundsPerTile, round R % kRoundsPerTile - 1)
+// into ring slot R % ZC_RING.  A round is ZC_ROUND = 128 bytes of each of the
+// wave's 64 rows; one instruction fills 8 rows (1 KiB); swizzle (row >> 1) & 7.
+__device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
+                                            uint32_t lane, uint64_t R, uint32_t grid) {
+  const uint64_t k = R / kRoundsPerTile;
+  const int r = (int)(R % kRoundsPerTile) - 1;
+  const uint64_t tile = blockIdx.x + k * grid;
+  uint8_t* slot = ring + (R % ZC_RING) * (64 * ZC_ROUND);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) cur[k] = p[k];
+  for (int j = 0; j < 64 * ZC_ROUND / 1024; ++j) {
+    const uint32_t row = j * (1024 / ZC_ROUND) + lane / (ZC_ROUND / 16);
+    const uint32_t p = (lane % (ZC_ROUND / 16)) ^ ((row >> 1) & 7);
+    const uint64_t span0 = tile * ZC_STILE + (uint64_t)(wave * 64 + row) * ZC_LSPAN;
+    const uint8_t* src = (r < 0 && span0 == 0) ? data + p * 16  // stream start: unused
+                                               : data + span0 + (int64_t)r * ZC_ROUND + p * 16;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(slot + j * 1024), 16, 0, 0);
+  }
+}
+
+template <int ABL>
+__global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t nfull, int32_t lo_thr,
+    uint64_t* __restrict__ blk, uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
+    uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list, uint32_t ovf_cap,
+    unsigned long long* __restrict__ counters) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
+  __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t grid = gridDim.x;
+  uint8_t* myring = ring[wave];
+  WaveList wl{wlist[wave], 0};
+  const uint64_t ntk = nfull > blockIdx.x ? (nfull - 1 - blockIdx.x) / grid + 1 : 0;
+  const uint64_t nR = ntk * kRoundsPerTile;
+  for (uint64_t R = 0; R < nR && R < ZC_RING - 1; ++R) stage_round(data, myring, wave, lane, R, grid);
+
+  ScanLane s{0, 0, 0};
+  const uint32_t sw = (lane >> 1) & 7;
 #pragma unroll 1
-      for (int bt = 0; bt < ZC_SPAN / 128; ++bt) {
-        if (bt + 1 < ZC_SPAN / 128) {
+  for (uint64_t R = 0; R < nR; ++R) {
+    if (R + ZC_RING - 1 < nR) {
+      stage_round(data, myring, wave, lane, R + ZC_RING - 1, grid);
+      wait_vmcnt<(64 * ZC_ROUND / 1024) * (ZC_RING - 1)>();  // round R's DMA has landed
+    } else {
+      wait_vmcnt<0>();
+    }
+    const uint64_t tile = blockIdx.x + (R / kRoundsPerTile) * grid;
+    const int r = (int)(R % kRoundsPerTile) - 1;
+    const uint64_t span0 = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
+    const uint8_t* row = myring + (R % ZC_RING) * (64 * ZC_ROUND) + lane * ZC_ROUND;
+    if (r < 0) {
+      // new tile: fresh lane state, gear warmed with the 32 bytes before the span
+      s = ScanLane{0, 0, 0};
+      wl.n = 0;
+      if (span0 >= 64) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) nxt[k] = p[(bt + 1) * 8 + k];
+        for (int p = (ZC_ROUND - 32) / 16; p < ZC_ROUND / 16; ++p) {
+          const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
+          const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t rel = bt * 128 + k * 16;
-          scan_dword<true>(cur[k].x, rel + 0, s, sl, cnt, span0);
-          scan_dword<true>(cur[k].y, rel + 4, s, sl, cnt, span0);
-          scan_dword<true>(cur[k].z, rel + 8, s, sl, cnt, span0);
-          scan_dword<true>(cur[k].w, rel + 12, s, sl, cnt, span0);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
       }
     } else {
-      // the stream's last, partial span
-      for (uint32_t i = 0; i < (uint32_t)len; ++i) {
-        uint32_t b = data[span0 + i];
-        gear_step(b, s);
-        digest_step(b, s);
-        if ((int32_t)s.glo >= ZC_ANCHOR_LO) record_anchor(sl, cnt, span0, i, s.glo, s.ghi);
+#pragma unroll
+      for (int p = 0; p < ZC_ROUND / 16; ++p) {
+        const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
+        const uint32_t rel = (uint32_t)r * ZC_ROUND + p * 16;
+        scan_dword<ABL>(v.x, rel + 0, lane, lo_thr, s, wl);
+        scan_dword<ABL>(v.y, rel + 4, lane, lo_thr, s, wl);
+        scan_dword<ABL>(v.z, rel + 8, lane, lo_thr, s, wl);
+        scan_dword<ABL>(v.w, rel + 12, lane, lo_thr, s, wl);
+      }
+      if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
+        blk[(span0 + (uint64_t)r * ZC_ROUND) / ZC_SPAN] = ((uint64_t)s.hhi << 32) | s.hlo;
+        s.hlo = s.hhi = 0;
+      }
+      if (r == ZC_LSPAN / ZC_ROUND - 1) {
+        // end of tile: move this wave's anchors to the per-span slots
+        const uint64_t sidx = span0 / ZC_LSPAN;
+        if (wl.n > ZC_WLIST) {
+          span_anchors_rescan(data, n, span0, lo_thr, false, blk, arel, ag, acnt, ovf_list, ovf_cap,
+                              counters);
+        } else {
+          uint32_t cnt = 0;
+          for (uint32_t i = 0; i < wl.n; ++i) {
+            const uint32_t e0 = wl.e[2 * i];
+            if ((e0 >> 16) == lane) {
+              const uint32_t rl = e0 & 0xFFFFu;
+              if (span0 + rl >= ZC_ANCHOR_MIN_OFF) {
+                if (cnt < ZC_ANC_SLOTS) {
+                  arel[sidx * ZC_ANC_SLOTS + cnt] = (uint16_t)rl;
+                  ag[sidx * ZC_ANC_SLOTS + cnt] = wl.e[2 * i + 1];
+                }
+                ++cnt;
+              }
+            }
+          }
+          acnt[sidx] = cnt;
+          if (cnt > ZC_ANC_SLOTS) {
+            unsigned long long k = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+            if (k < ovf_cap) {
+              ovf_list[2 * k] = (uint32_t)sidx;
+              ovf_list[2 * k + 1] = cnt;
+            }
+          }
+          if (cnt) atomicAdd(&counters[CNT_POOL], (unsigned long long)cnt);
+        }
       }
     }
-    blk[span0 / ZC_SPAN] = ((uint64_t)s.hhi << 32) | s.hlo;
   }
+}
 
-  // ordered compaction of the tile's anchors (lane order, then position)
-  uint32_t total;
-  uint32_t off = block_excl_scan(cnt, s_tmp, total);
-  if (tid == 0) {
-    uint64_t base = total ? atomicAdd(&counters[CNT_POOL], (unsigned long long)total) : 0;
-    if (base + total > pool_cap) atomicOr(&counters[CNT_OVERFLOW], 1ull);
-    tile_off[tile] = base;
-    tile_cnt[tile] = total;
-    s_base = base;
-  }
-  __syncthreads();
-  const uint64_t base = s_base;
-  if (cnt == 0 || base + total > pool_cap) return;
-  Anchor* dst = pool + base + off;
-  if (cnt <= ZC_LANE_SLOTS) {
-    for (uint32_t i = 0; i < cnt; ++i) {
-      uint32_t r = sl.rel[i * ZC_TPB];
-      dst[i].pos = span0 + r;
-      dst[i].fp = ((uint64_t)sl.ghi[i * ZC_TPB] << 32) | sl.glo[i * ZC_TPB];
+// the stream's last, partial tile: bytewise, one lane per span
+__global__ void __launch_bounds__(ZC_SCAN_TPB) zc_scan_tail_kernel(
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile, int32_t lo_thr,
+    uint64_t* __restrict__ blk, uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
+    uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list, uint32_t ovf_cap,
+    unsigned long long* __restrict__ counters) {
+  const uint64_t span0 = tile * ZC_STILE + (uint64_t)threadIdx.x * ZC_LSPAN;
+  if (span0 >= n) return;
+  span_anchors_rescan(data, n, span0, lo_thr, true, blk, arel, ag, acnt, ovf_list, ovf_cap, counters);
+}
+
+// rescan of lane spans whose anchors overflowed their slots: every anchor is
+// written, in order, to the overflow pool at offs[i]; ovf_off[span] = offs[i]
+__global__ void zc_anchor_dense_kernel(const uint8_t* __restrict__ data, uint64_t n, int32_t lo_thr,
+                                       const uint32_t* __restrict__ spans, uint32_t nspans,
+                                       const uint64_t* __restrict__ offs, uint64_t* __restrict__ ovf_off,
+                                       uint16_t* __restrict__ orel, uint32_t* __restrict__ og) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nspans) return;
+  const uint64_t sidx = spans[i];
+  const uint64_t span0 = sidx * ZC_LSPAN;
+  ScanLane s{0, 0, 0};
+  if (span0 >= 64)
+    for (uint64_t q = span0 - 64; q < span0; ++q) gear_step(data[q], s);
+  const uint64_t end = (span0 + ZC_LSPAN < n) ? span0 + ZC_LSPAN : n;
+  uint64_t w = offs[i];
+  ovf_off[sidx] = w;
+  for (uint64_t p = span0; p < end; ++p) {
+    gear_step(data[p], s);
+    if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) {
+      orel[w] = (uint16_t)(p - span0);
+      og[w] = s.glo;
+      ++w;
     }
-  } else {
-    // more anchors than LDS slots (never for random data): rescan the span
-    ScanLane s{0, 0, 0, 0};
-    gear_warm(data, span0, s);
-    const uint64_t len = (n - span0 < ZC_SPAN) ? (n - span0) : ZC_SPAN;
-    uint32_t w = 0;
-    for (uint32_t i = 0; i < (uint32_t)len; ++i) {
-      gear_step(data[span0 + i], s);
-      if ((int32_t)s.glo >= ZC_ANCHOR_LO && span0 + i >= ZC_ANCHOR_MIN_OFF) {
-        dst[w].pos = span0 + i;
-        dst[w].fp = ((uint64_t)s.ghi << 32) | s.glo;
-        ++w;
-      }
-    }
   }
+}
+
+// the anchors of lane span `sidx`: pointers + count
+struct SpanAnchors {
+  const uint16_t* rel;
+  const uint32_t* g;
+  uint32_t cnt;
+};
+
+__device__ __forceinline__ SpanAnchors span_anchors(const AnchorView& av, uint64_t sidx) {
+  uint32_t c = av.cnt[sidx];
+  if (c <= ZC_ANC_SLOTS) return SpanAnchors{av.rel + sidx * ZC_ANC_SLOTS, av.g + sidx * ZC_ANC_SLOTS, c};
+  const uint64_t o = av.ovf_off[sidx];
+  return SpanAnchors{av.orel + o, av.og + o, c};
 }
 
 // ---------------------------------------------------------------------------
-// zc_chunk_meta: thread per chunk [start, start+W)
+// zc_chunk_meta: thread per chunk [start, start+W): key, first anchor (offset,
+// gear value, 64-byte fingerprint)
 __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
-                                     const uint64_t* __restrict__ blk, const Anchor* __restrict__ pool,
-                                     const uint64_t* __restrict__ tile_off,
-                                     const uint32_t* __restrict__ tile_cnt,
+                                     const uint64_t* __restrict__ blk, AnchorView av,
                                      const uint64_t* __restrict__ starts, uint32_t nchunks, uint32_t W,
-                                     uint64_t pw, uint64_t* __restrict__ key, uint64_t* __restrict__ fp,
-                                     uint32_t* __restrict__ anc_off) {
+                                     uint64_t pw, uint64_t* __restrict__ key, uint32_t* __restrict__ cg,
+                                     uint64_t* __restrict__ cfp, uint32_t* __restrict__ anc_off) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nchunks) return;
   const uint64_t c = starts[i];
   key[i] = pw + rk_acc(data, blk, c, c + W);
-  uint32_t off = ZC_NO_ANCHOR;
+  uint32_t off = ZC_NO_ANCHOR, gv = 0;
   uint64_t f = 0;
   if (W > ZC_ANCHOR_MIN_OFF) {
     const uint64_t lo = c + ZC_ANCHOR_MIN_OFF, hi = c + W - 1;  // inclusive
-    for (uint64_t t = lo / ZC_TILE; t <= hi / ZC_TILE; ++t) {
-      const Anchor* a = pool + tile_off[t];
-      uint32_t m = tile_cnt[t];
-      uint32_t L = 0, R = m;  // first entry with pos >= lo
+    for (uint64_t sx = lo / ZC_LSPAN; sx <= hi / ZC_LSPAN; ++sx) {
+      SpanAnchors sa = span_anchors(av, sx);
+      const uint32_t lo_rel = (sx == lo / ZC_LSPAN) ? (uint32_t)(lo - sx * ZC_LSPAN) : 0;
+      uint32_t L = 0, R = sa.cnt;  // first entry with rel >= lo_rel
       while (L < R) {
         uint32_t mid = (L + R) >> 1;
-        if (a[mid].pos < lo) L = mid + 1; else R = mid;
+        if (sa.rel[mid] < lo_rel) L = mid + 1; else R = mid;
       }
-      if (L < m) {
-        if (a[L].pos <= hi) {
-          off = (uint32_t)(a[L].pos - c);
-          f = a[L].fp;
+      if (L < sa.cnt) {
+        const uint64_t pos = sx * ZC_LSPAN + sa.rel[L];
+        if (pos <= hi) {
+          off = (uint32_t)(pos - c);
+          gv = sa.g[L];
+          f = anchor_fp(data, pos);
         }
-        break;  // anchors of later tiles are beyond this one
+        break;  // later spans only hold later anchors
       }
     }
   }
   anc_off[i] = off;
-  fp[i] = f;
+  cg[i] = gv;
+  cfp[i] = f;
 }
 
 // ---------------------------------------------------------------------------
-// anchor table: open addressing on the 64-bit fingerprint, duplicates kept
+// anchor table: open addressing on the anchor's gear value, duplicates kept;
+// the 64-bit fingerprint is compared on a hit
 constexpr uint64_t kEmpty = ~0ull;
-
-__device__ __forceinline__ uint64_t table_key(uint64_t fp) { return fp == kEmpty ? kEmpty - 1 : fp; }
 
 __global__ void zc_table_clear_kernel(uint64_t* tkeys, uint32_t tsize) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < tsize) tkeys[i] = kEmpty;
 }
 
+__device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
+  return (uint32_t)(((uint64_t)g * kGolden) >> (64 - tbits));
+}
+
 __global__ void zc_table_insert_kernel(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,
-                                       const uint64_t* __restrict__ fp,
+                                       const uint32_t* __restrict__ cg,
                                        const uint32_t* __restrict__ anc_off, uint32_t nrefs) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nrefs || anc_off[i] == ZC_NO_ANCHOR) return;
-  const uint64_t k = table_key(fp[i]);
+  const uint64_t k = cg[i];
   const uint32_t mask = (1u << tbits) - 1;
-  uint32_t h = (uint32_t)((k * kGolden) >> (64 - tbits));
+  uint32_t h = table_slot(cg[i], tbits);
   for (;;) {
     unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[h], (unsigned long long)kEmpty,
                                         (unsigned long long)k);
@@ -355,40 +554,51 @@ __global__ void zc_table_insert_kernel(uint64_t* tkeys, uint32_t* tvals, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// zc_probe: thread per anchor of the stream
-__global__ void zc_probe_kernel(const Anchor* __restrict__ pool, uint64_t npool,
+// zc_probe: thread per lane span; every anchor probes the table
+__global__ void zc_probe_kernel(const uint8_t* __restrict__ data, AnchorView av, uint64_t nspans,
                                 const uint64_t* __restrict__ tkeys, const uint32_t* __restrict__ tvals,
-                                uint32_t tbits, const uint64_t* __restrict__ chunk_start,
-                                const uint32_t* __restrict__ anc_off, const uint64_t* __restrict__ vis,
+                                uint32_t tbits, const uint32_t* __restrict__ anc_off,
+                                const uint64_t* __restrict__ cfp, const uint64_t* __restrict__ vis,
                                 const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W,
                                 Cand* __restrict__ cand, uint64_t cand_cap,
                                 unsigned long long* __restrict__ counters) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npool) return;
-  const Anchor a = pool[i];
-  if (a.pos < r + ZC_ANCHOR_MIN_OFF) return;
-  const uint64_t k = table_key(a.fp);
+  uint64_t sx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sx >= nspans) return;
+  SpanAnchors sa = span_anchors(av, sx);
   const uint32_t mask = (1u << tbits) - 1;
-  uint32_t h = (uint32_t)((k * kGolden) >> (64 - tbits));
-  for (;;) {
-    uint64_t tk = tkeys[h];
-    if (tk == kEmpty) break;
-    if (tk == k) {
-      uint32_t ref = tvals[h];
-      uint64_t o = anc_off[ref];
-      if (a.pos >= r + o) {
-        uint64_t ws = a.pos - o, p = ws + W - 1;
-        if (p < n && p >= vis[ref] && !dead[ref]) {
-          unsigned long long slot = atomicAdd(&counters[CNT_CAND], 1ull);
-          if (slot < cand_cap) {
-            cand[slot].p = p;
-            cand[slot].ref = ref;
-            cand[slot].pad = 0;
+  for (uint32_t e = 0; e < sa.cnt; ++e) {
+    const uint64_t pos = sx * ZC_LSPAN + sa.rel[e];
+    if (pos < r + ZC_ANCHOR_MIN_OFF) continue;
+    const uint64_t k = sa.g[e];
+    uint32_t h = table_slot(sa.g[e], tbits);
+    bool have_fp = false;
+    uint64_t fp = 0;
+    for (;;) {
+      uint64_t tk = tkeys[h];
+      if (tk == kEmpty) break;
+      if (tk == k) {
+        uint32_t ref = tvals[h];
+        uint64_t o = anc_off[ref];
+        if (pos >= r + o) {
+          uint64_t ws = pos - o, p = ws + W - 1;
+          if (p < n && p >= vis[ref] && !dead[ref]) {
+            if (!have_fp) {
+              fp = anchor_fp(data, pos);
+              have_fp = true;
+            }
+            if (fp == cfp[ref]) {
+              unsigned long long slot = atomicAdd(&counters[CNT_CAND], 1ull);
+              if (slot < cand_cap) {
+                cand[slot].p = p;
+                cand[slot].ref = ref;
+                cand[slot].pad = 0;
+              }
+            }
           }
         }
       }
+      h = (h + 1) & mask;
     }
-    h = (h + 1) & mask;
   }
 }
 
@@ -543,7 +753,7 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
   if (!fits || s_over) {
     if (tid == 0) {
       uint64_t base = atomicAdd(&counters[CNT_RUNS], (unsigned long long)total);
-      if (base + total > runs_cap) atomicOr(&counters[CNT_OVERFLOW], 2ull);
+      if (base + total > runs_cap) atomicOr(&counters[CNT_FOVF], 1ull);
       tile_off[tile] = base;
       tile_cnt[tile] = total;
       s_base = base;
@@ -587,7 +797,7 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
   head_ex = block_excl_scan(my_heads, s_tmp, nheads);
   if (tid == 0) {
     uint64_t base = atomicAdd(&counters[CNT_RUNS], (unsigned long long)nheads);
-    if (base + nheads > runs_cap) atomicOr(&counters[CNT_OVERFLOW], 2ull);
+    if (base + nheads > runs_cap) atomicOr(&counters[CNT_FOVF], 1ull);
     tile_off[tile] = base;
     tile_cnt[tile] = nheads;
     s_base = base;
@@ -714,23 +924,47 @@ inline unsigned blocks_for(uint64_t items, unsigned per) { return (unsigned)((it
 
 uint64_t pow257(uint64_t e) { return pow257_dev(e); }
 
-hipError_t launch_scan(const uint8_t* data, uint64_t n, uint64_t* blk, Anchor* pool,
-                       uint64_t pool_cap, uint64_t* tile_off, uint32_t* tile_cnt,
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, uint16_t* arel,
+                       uint32_t* ag, uint32_t* acnt, uint32_t* ovf_list, uint32_t ovf_cap,
                        unsigned long long* counters, hipStream_t s) {
-  uint64_t ntiles = (n + ZC_TILE - 1) / ZC_TILE;
-  if (!ntiles) return hipSuccess;
-  hipLaunchKernelGGL(zc_scan_kernel, dim3((unsigned)ntiles), dim3(ZC_TPB), 0, s, data, n, blk, pool,
-                     pool_cap, tile_off, tile_cnt, counters);
+  const uint64_t nfull = n / ZC_STILE;
+  if (nfull) {
+    const unsigned grid = (unsigned)std::min<uint64_t>(nfull, (uint64_t)cu_count());
+    hipLaunchKernelGGL(zc_scan_kernel<0>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, nfull, anchor_lo, blk,
+                       arel, ag, acnt, ovf_list, ovf_cap, counters);
+  }
+  if (n % ZC_STILE)
+    hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(1), dim3(ZC_SCAN_TPB), 0, s, data, n, nfull, anchor_lo, blk,
+                       arel, ag, acnt, ovf_list, ovf_cap, counters);
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk,
-                             const Anchor* pool, const uint64_t* tile_off, const uint32_t* tile_cnt,
+hipError_t launch_anchor_dense(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* spans,
+                               uint32_t nspans, const uint64_t* offs, uint64_t* ovf_off, uint16_t* orel,
+                               uint32_t* og, hipStream_t s) {
+  if (!nspans) return hipSuccess;
+  hipLaunchKernelGGL(zc_anchor_dense_kernel, dim3(blocks_for(nspans, 64)), dim3(64), 0, s, data, n, anchor_lo,
+                     spans, nspans, offs, ovf_off, orel, og);
+  return hipGetLastError();
+}
+
+hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av,
                              const uint64_t* starts, uint32_t nchunks, uint32_t W, uint64_t pw,
-                             uint64_t* key, uint64_t* fp, uint32_t* anc_off, hipStream_t s) {
+                             uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off, hipStream_t s) {
   if (!nchunks) return hipSuccess;
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(nchunks, 128)), dim3(128), 0, s, data, n,
-                     blk, pool, tile_off, tile_cnt, starts, nchunks, W, pw, key, fp, anc_off);
+                     blk, av, starts, nchunks, W, pw, key, cg, cfp, anc_off);
   return hipGetLastError();
 }
 
@@ -739,22 +973,21 @@ hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits, const uint64_t* fp,
+hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits, const uint32_t* cg,
                                const uint32_t* anc_off, uint32_t nrefs, hipStream_t s) {
   if (!nrefs) return hipSuccess;
   hipLaunchKernelGGL(zc_table_insert_kernel, dim3(blocks_for(nrefs, 256)), dim3(256), 0, s, tkeys,
-                     tvals, tbits, fp, anc_off, nrefs);
+                     tvals, tbits, cg, anc_off, nrefs);
   return hipGetLastError();
 }
 
-hipError_t launch_probe(const Anchor* pool, uint64_t npool, const uint64_t* tkeys,
-                        const uint32_t* tvals, uint32_t tbits, const uint64_t* chunk_start,
-                        const uint32_t* anc_off, const uint64_t* vis, const uint8_t* dead,
-                        uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
-                        unsigned long long* counters, hipStream_t s) {
-  if (!npool) return hipSuccess;
-  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(npool, 256)), dim3(256), 0, s, pool, npool, tkeys,
-                     tvals, tbits, chunk_start, anc_off, vis, dead, r, n, W, cand, cand_cap, counters);
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nspans, const uint64_t* tkeys,
+                        const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp,
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t n, uint32_t W,
+                        Cand* cand, uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
+  if (!nspans) return hipSuccess;
+  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(nspans, 256)), dim3(256), 0, s, data, av, nspans,
+                     tkeys, tvals, tbits, anc_off, cfp, vis, dead, r, n, W, cand, cand_cap, counters);
   return hipGetLastError();
 }
 
