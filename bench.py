@@ -167,7 +167,10 @@ def main():
                          "scan_ms_avg": round(scan_avg, 4)},
             "stages": {"scan_ms": round(st["scan_ms"], 4), "resolve_ms": round(st["resolve_ms"], 4),
                        "total_ms": round(st["total_ms"], 4), "anchors": st["anchors"],
-                       "candidates": st["candidates"], "epochs": st["epochs"]},
+                       "candidates": st["candidates"], "epochs": st["epochs"],
+                       "meta_ms": round(st["meta_ms"], 4), "probe_ms": round(st["probe_ms"], 4),
+                       "fscan_ms": round(st["fscan_ms"], 4), "walk_ms": round(st["walk_ms"], 4),
+                       "finalize_ms": round(st["finalize_ms"], 4)},
         }
         if e2e:
             out["end_to_end"] = e2e

@@ -82,6 +82,11 @@ typedef struct {
   uint64_t candidates;   /* anchor-probe candidates */
   uint64_t epochs;       /* resolution epochs (1 + grid-shifting matches) */
   uint64_t fscan_runs;   /* screen-hit runs from the exact-hash screen */
+  double meta_ms;        /* grid-chunk keys + first anchors (wall clock, summed over epochs) */
+  double probe_ms;       /* anchor table + probe + candidate verification */
+  double fscan_ms;       /* exact-hash screen */
+  double walk_ms;        /* boundary walk + record assembly on the host */
+  double finalize_ms;    /* digests of cut pieces, SHA-1 ids */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;
@@ -99,7 +104,9 @@ int zc_feed(zc_ctx* ctx, const void* host, size_t n); /* copying convenience for
 int zc_finish(zc_ctx* ctx);
 
 /* device-resident stream: d_data is a device pointer on the context's GPU,
- * 16-byte aligned; the call runs the whole pipeline and fills the records */
+ * 16-byte aligned; the call runs the whole pipeline and fills the records.
+ * The context's stream is ordered after work already queued on the legacy
+ * default stream (so a buffer just written there is read complete). */
 int zc_chunk_device(zc_ctx* ctx, const void* d_data, uint64_t n);
 
 size_t zc_record_count(const zc_ctx* ctx);

@@ -34,7 +34,10 @@ class ZcStats(ctypes.Structure):
     _fields_ = [("scan_ms", ctypes.c_double), ("resolve_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("bytes", ctypes.c_uint64),
                 ("anchors", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
-                ("epochs", ctypes.c_uint64), ("fscan_runs", ctypes.c_uint64)]
+                ("epochs", ctypes.c_uint64), ("fscan_runs", ctypes.c_uint64),
+                ("meta_ms", ctypes.c_double), ("probe_ms", ctypes.c_double),
+                ("fscan_ms", ctypes.c_double), ("walk_ms", ctypes.c_double),
+                ("finalize_ms", ctypes.c_double)]
 
 
 class ZcError(RuntimeError):

@@ -68,7 +68,8 @@ struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
 // Counters word layout (uint64 each)
 // CNT_POOL: anchors found; CNT_OVERFLOW: lane spans over ZC_ANC_SLOTS anchors;
 // CNT_FOVF: screen-run buffer overflow flag
-enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_LAST = 8 };
+// CNT_ANCLESS: refs without an anchor
+enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_ANCLESS = 5, CNT_LAST = 8 };
 
 // --- launchers (return hipError_t of the launch) ---------------------------
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, uint16_t* arel,
@@ -82,9 +83,14 @@ hipError_t launch_anchor_dense(const uint8_t* data, uint64_t n, int32_t anchor_l
                                uint32_t nspans, const uint64_t* offs, uint64_t* ovf_off, uint16_t* orel,
                                uint32_t* og, hipStream_t s);
 
-hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av,
-                             const uint64_t* starts, uint32_t nchunks, uint32_t W, uint64_t pw,
-                             uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off, hipStream_t s);
+// grid chunks i < nchunks of an epoch starting at r_e (start = r_e + i * W)
+hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
+                             uint32_t nchunks, uint32_t W, uint64_t pw, uint64_t* start, uint64_t* vis,
+                             uint8_t* dead, uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off,
+                             hipStream_t s);
+
+hipError_t launch_anchorless(const uint32_t* anc_off, uint32_t nref, uint32_t* list, uint32_t cap,
+                             unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s);
 hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,

@@ -39,6 +39,11 @@ using namespace zc;
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
+}
+
 struct ZcError {
   int code;
   std::string msg;
@@ -78,6 +83,36 @@ struct DevBuf {
   }
 };
 
+// pinned host memory: device->host copies land here without a bounce
+template <class T>
+struct HostBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  void ensure(size_t n) {
+    if (n <= cap && p) return;
+    release();
+    size_t want = std::max<size_t>(n, 1);
+    hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      throw ZcError{ZC_ERR_NOMEM, std::string("hipHostMalloc(") + std::to_string(want * sizeof(T)) +
+                                      "): " + hipGetErrorString(e)};
+    }
+    cap = want;
+  }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+};
+
 struct StaticEntry {
   uint64_t key;
   uint8_t sha[16];
@@ -94,7 +129,7 @@ struct zc_ctx {
   uint32_t W = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_in = nullptr;
   std::string err;
 
   // host feed
@@ -128,6 +163,9 @@ struct zc_ctx {
   DevBuf<uint8_t> vok, sha_out;
   DevBuf<uint32_t> f32, fbits;
   DevBuf<Run> runs;
+  DevBuf<uint32_t> ancless;
+  HostBuf<unsigned long long> h_cnt;
+  HostBuf<uint64_t> h_key;  // grid-chunk keys of the current epoch
 };
 
 namespace {
@@ -162,6 +200,7 @@ class Resolver {
   void run() {
     auto t0 = std::chrono::steady_clock::now();
     c_.recs.clear();
+    c_.recs.reserve(std::min<uint64_t>(n_ / W_ + 16, 1u << 24));
     c_.stats = zc_stats{};
     c_.stats.bytes = n_;
     if (n_ == 0) return;
@@ -194,12 +233,20 @@ class Resolver {
   uint64_t r_ = 0, s_ = 0, r_e_ = 0;
 
   // refs = indexable W-byte chunks that can be matched: [0, nconf_) saved in
-  // earlier epochs, [nconf_, nconf_+nspec_) this epoch's grid chunks
-  std::vector<uint64_t> start_, key_, fp_, vis_;  // fp_: 64-byte anchor fingerprint
-  std::vector<uint32_t> anc_, g_;                  // g_: anchor gear value
+  // earlier epochs (visible to every later probe), [nconf_, nref_) this
+  // epoch's grid chunks, start r_e + k * W, visible from start + 2W - 1.
+  // The grid chunks' metadata lives on the device; the host holds their keys.
+  std::vector<uint64_t> cstart_, ckey_, cfp_;  // cfp_: 64-byte anchor fingerprint
+  std::vector<uint32_t> canc_, cg_;            // cg_: anchor gear value
   std::vector<uint8_t> dead_;
-  uint32_t nconf_ = 0, nspec_ = 0;
+  uint32_t nconf_ = 0, nspec_ = 0, nref_ = 0;
   uint64_t ks_ = 0;  // next grid chunk of this epoch to save
+
+  uint64_t ref_start(uint32_t ref) const {
+    return ref < nconf_ ? cstart_[ref] : r_e_ + (uint64_t)(ref - nconf_) * W_;
+  }
+  uint64_t ref_vis(uint32_t ref) const { return ref < nconf_ ? 0 : ref_start(ref) + 2ull * W_ - 1; }
+  uint64_t ref_key(uint32_t ref) const { return ref < nconf_ ? ckey_[ref] : c_.h_key[ref - nconf_]; }
 
   std::unordered_map<uint64_t, std::vector<uint32_t>> fmap_;  // key -> anchorless refs (start order)
   std::unordered_map<uint64_t, std::vector<uint32_t>> smap_;  // key -> statics
@@ -303,102 +350,117 @@ class Resolver {
   }
 
   // ---------------------------------------------------------------- epoch
+  // One epoch = one grid origin r_e.  Device work is queued back to back
+  // (grid-chunk metadata, anchor table, probe, anchorless compaction) and read
+  // back with one synchronisation.
   bool epoch() {
     c_.stats.epochs++;
     r_e_ = r_;
     s_ = r_;
     ks_ = 0;
     nspec_ = (n_ >= r_e_ + 2ull * W_) ? (uint32_t)((n_ - r_e_ - 2ull * W_) / W_ + 1) : 0;
-    const uint32_t nrefs_spec = indexable_ ? nspec_ : 0;
-    const uint32_t nref = nconf_ + nrefs_spec;
-    start_.resize(nref);
-    key_.resize(nref);
-    fp_.resize(nref);
-    g_.resize(nref);
-    vis_.resize(nref);
-    anc_.resize(nref);
-    dead_.assign(nref, 0);
-    for (uint32_t k = 0; k < nrefs_spec; ++k) {
-      start_[nconf_ + k] = r_e_ + (uint64_t)k * W_;
-      vis_[nconf_ + k] = start_[nconf_ + k] + 2ull * W_ - 1;
-    }
+    const uint32_t nsref = indexable_ ? nspec_ : 0;
+    nref_ = nconf_ + nsref;
+    dead_.assign(nref_, 0);
     acands_.clear();
     runs_.clear();
     fmap_.clear();
     fb_ = FBatch{};
     has_f_ = false;
     f_min_vis_ = kInf;
-    if (nref) {
-      c_.c_start.ensure(nref);
-      c_.c_key.ensure(nref);
-      c_.c_fp.ensure(nref);
-      c_.c_vis.ensure(nref);
-      c_.c_anc.ensure(nref);
-      c_.c_g.ensure(nref);
-      c_.c_dead.ensure(nref);
-      h2d(c_, c_.c_start.p, start_.data(), nref);
-      h2d(c_, c_.c_key.p, key_.data(), nconf_);
-      h2d(c_, c_.c_fp.p, fp_.data(), nconf_);
-      h2d(c_, c_.c_anc.p, anc_.data(), nconf_);
-      h2d(c_, c_.c_g.p, g_.data(), nconf_);
-      h2d(c_, c_.c_vis.p, vis_.data(), nref);
-      h2d(c_, c_.c_dead.p, dead_.data(), nref);
-      HCK(launch_chunk_meta(d_, n_, c_.blk.p, av_, c_.c_start.p + nconf_,
-                            nrefs_spec, W_, pow257(W_), c_.c_key.p + nconf_, c_.c_g.p + nconf_,
-                            c_.c_fp.p + nconf_, c_.c_anc.p + nconf_, c_.stream));
-      d2h(c_, key_.data() + nconf_, c_.c_key.p + nconf_, nrefs_spec);
-      d2h(c_, fp_.data() + nconf_, c_.c_fp.p + nconf_, nrefs_spec);
-      d2h(c_, anc_.data() + nconf_, c_.c_anc.p + nconf_, nrefs_spec);
-      d2h(c_, g_.data() + nconf_, c_.c_g.p + nconf_, nrefs_spec);
+    uint64_t ncand = 0, nancless = 0;
+    if (nref_) {
+      auto tm = Clock::now();
+      c_.c_start.ensure(nref_);
+      c_.c_key.ensure(nref_);
+      c_.c_fp.ensure(nref_);
+      c_.c_vis.ensure(nref_);
+      c_.c_anc.ensure(nref_);
+      c_.c_g.ensure(nref_);
+      c_.c_dead.ensure(nref_);
+      c_.ancless.ensure(nref_);
+      c_.h_key.ensure(nsref);
+      c_.h_cnt.ensure(CNT_LAST);
+      if (nconf_) {
+        h2d(c_, c_.c_start.p, cstart_.data(), nconf_);
+        h2d(c_, c_.c_key.p, ckey_.data(), nconf_);
+        h2d(c_, c_.c_fp.p, cfp_.data(), nconf_);
+        h2d(c_, c_.c_anc.p, canc_.data(), nconf_);
+        h2d(c_, c_.c_g.p, cg_.data(), nconf_);
+        HCK(hipMemsetAsync(c_.c_vis.p, 0, nconf_ * sizeof(uint64_t), c_.stream));
+        HCK(hipMemsetAsync(c_.c_dead.p, 0, nconf_, c_.stream));
+      }
+      HCK(launch_chunk_meta(d_, n_, c_.blk.p, av_, r_e_, nsref, W_, pow257(W_), c_.c_start.p + nconf_,
+                            c_.c_vis.p + nconf_, c_.c_dead.p + nconf_, c_.c_key.p + nconf_,
+                            c_.c_g.p + nconf_, c_.c_fp.p + nconf_, c_.c_anc.p + nconf_, c_.stream));
+      HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+      uint32_t tbits = 10;  // sized for every ref having an anchor
+      while ((1u << tbits) < 2u * nref_) ++tbits;
+      if (npool_) {
+        c_.tkeys.ensure(1u << tbits);
+        c_.tvals.ensure(1u << tbits);
+        c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
+        HCK(launch_table_clear(c_.tkeys.p, 1u << tbits, c_.stream));
+        HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_g.p, c_.c_anc.p, nref_, c_.stream));
+        HCK(launch_probe(d_, av_, nls_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
+                         c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+      }
+      HCK(launch_anchorless(c_.c_anc.p, nref_, c_.ancless.p, nref_, c_.counters.p, c_.stream));
+      d2h(c_, c_.h_key.p, c_.c_key.p + nconf_, nsref);
+      d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
-      probe_anchors(nref);
+      ncand = c_.h_cnt[CNT_CAND];
+      nancless = c_.h_cnt[CNT_ANCLESS];
+      if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
+        c_.cand.ensure(ncand + 1024);
+        HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
+        HCK(launch_probe(d_, av_, nls_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
+                         c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
+        sync(c_);
+        ncand = c_.h_cnt[CNT_CAND];
+        if (ncand > c_.cand.cap) throw ZcError{ZC_ERR_NOMEM, "candidate buffer overflow persisted"};
+      }
+      c_.stats.meta_ms += ms_since(tm);
+    }
+    if (ncand) {
+      auto tp = Clock::now();
+      verify_candidates(ncand);
+      c_.stats.probe_ms += ms_since(tp);
     }
     // keys without an anchor, and the static index, go through the exact screen
-    for (uint32_t i = 0; i < nref; ++i)
-      if (anc_[i] == ZC_NO_ANCHOR) {
-        fmap_[key_[i]].push_back(i);
-        f_min_vis_ = std::min(f_min_vis_, vis_[i]);
+    if (nancless) {
+      std::vector<uint32_t> refs(nancless);
+      d2h(c_, refs.data(), c_.ancless.p, nancless);
+      sync(c_);
+      std::sort(refs.begin(), refs.end());  // start order within each key
+      for (uint32_t ref : refs) {
+        fmap_[ref_key(ref)].push_back(ref);
+        f_min_vis_ = std::min(f_min_vis_, ref_vis(ref));
       }
+    }
     if (!smap_.empty()) f_min_vis_ = 0;
-    if (!fmap_.empty() || !smap_.empty()) fscan();
-    return walk();
+    if (!fmap_.empty() || !smap_.empty()) {
+      auto tf = Clock::now();
+      fscan();
+      c_.stats.fscan_ms += ms_since(tf);
+    }
+    auto tw = Clock::now();
+    bool again = walk();
+    c_.stats.walk_ms += ms_since(tw);
+    return again;
   }
 
-  void probe_anchors(uint32_t nref) {
-    uint32_t nanc = 0;
-    for (uint32_t i = 0; i < nref; ++i) nanc += anc_[i] != ZC_NO_ANCHOR;
-    if (!nanc || !npool_) return;
-    uint32_t tbits = 10;
-    while ((1u << tbits) < 2u * nanc) ++tbits;
-    const uint32_t tsize = 1u << tbits;
-    c_.tkeys.ensure(tsize);
-    c_.tvals.ensure(tsize);
-    HCK(launch_table_clear(c_.tkeys.p, tsize, c_.stream));
-    HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_g.p, c_.c_anc.p, nref, c_.stream));
-    uint64_t cap = std::max<uint64_t>(1u << 16, nanc);
-    unsigned long long cnt[CNT_LAST];
-    for (int attempt = 0; attempt < 3; ++attempt) {
-      c_.cand.ensure(cap);
-      HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-      HCK(launch_probe(d_, av_, nls_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p, c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p,
-                       c_.stream));
-      d2h(c_, cnt, c_.counters.p, CNT_LAST);
-      sync(c_);
-      if (cnt[CNT_CAND] <= c_.cand.cap) break;
-      cap = cnt[CNT_CAND] + 1024;
-      if (attempt == 2) throw ZcError{ZC_ERR_NOMEM, "candidate buffer overflow persisted"};
-    }
-    const uint64_t nc = cnt[CNT_CAND];
+  // byte-exact verification of every probe candidate window against its chunk
+  void verify_candidates(uint64_t nc) {
     c_.stats.candidates += nc;
-    if (!nc) return;
     std::vector<Cand> hc(nc);
     d2h(c_, hc.data(), c_.cand.p, nc);
     sync(c_);
-    // byte-exact verification of every candidate window against its chunk
     std::vector<uint64_t> wa(nc), ra(nc);
     for (uint64_t i = 0; i < nc; ++i) {
       wa[i] = hc[i].p - W_ + 1;
-      ra[i] = start_[hc[i].ref];
+      ra[i] = ref_start(hc[i].ref);
     }
     std::vector<uint8_t> ok = verify_pairs(wa, ra, W_);
     acands_.reserve(nc);
@@ -522,7 +584,7 @@ class Resolver {
     auto it = fmap_.find(h);
     if (it == fmap_.end()) return -1;
     for (uint32_t ref : it->second) {
-      if (vis_[ref] > p) break;
+      if (ref_vis(ref) > p) break;
       if (!dead_[ref]) return ref;
     }
     return -1;
@@ -574,7 +636,7 @@ class Resolver {
       if (ref >= 0) {
         b.vref[i] = ref;
         wa.push_back(a[i]);
-        ra.push_back(start_[ref]);
+        ra.push_back(ref_start(ref));
         widx.push_back(i);
       }
       if (smap_.count(b.h[i])) {
@@ -604,13 +666,13 @@ class Resolver {
     auto it = fmap_.find(h);
     if (it != fmap_.end()) {
       for (uint32_t ref : it->second) {
-        if (vis_[ref] > p) break;
+        if (ref_vis(ref) > p) break;
         if (dead_[ref]) continue;
         bool ok;
         if (fb_.vref[i] == (int64_t)ref) {
           ok = fb_.vok[i];
         } else {
-          std::vector<uint64_t> wa{p - W_ + 1}, ra{start_[ref]};
+          std::vector<uint64_t> wa{p - W_ + 1}, ra{ref_start(ref)};
           ok = verify_pairs(wa, ra, W_)[0];
         }
         if (ok) return true;
@@ -644,7 +706,7 @@ class Resolver {
   }
 
   // ---------------------------------------------------------------- walk
-  bool alive_visible(uint32_t ref, uint64_t p) const { return vis_[ref] <= p && !dead_[ref]; }
+  bool alive_visible(uint32_t ref, uint64_t p) const { return ref_vis(ref) <= p && !dead_[ref]; }
 
   void push(uint64_t off, uint32_t size, uint32_t kind, uint64_t rolling) {
     zc_record r;
@@ -675,7 +737,7 @@ class Resolver {
       const bool dead = indexable_ && dead_[nconf_ + ks_];
       if (!dead && ck >= s_) {
         if (indexable_) {
-          push(ck, W_, ZC_CHUNK_NEW, key_[nconf_ + ks_]);
+          push(ck, W_, ZC_CHUNK_NEW, c_.h_key[ks_]);
         } else {
           push(ck, W_, ZC_BYTES, 0);
         }
@@ -729,7 +791,7 @@ class Resolver {
         key = fkey;
       } else {
         m = pa;
-        key = key_[refa];
+        key = ref_key(refa);
       }
       // the match at m
       save_grid_until(m);
@@ -747,26 +809,45 @@ class Resolver {
         continue;
       }
       // grid shift: keep the saved chunks of this epoch, start a new one
-      std::vector<uint32_t> keep;
-      for (uint32_t k = 0; k < (indexable_ ? nspec_ : 0); ++k) {
-        uint32_t ref = nconf_ + k;
-        if (!dead_[ref] && vis_[ref] <= m) keep.push_back(ref);
-      }
-      for (uint32_t ref : keep) {
-        start_[nconf_] = start_[ref];
-        key_[nconf_] = key_[ref];
-        fp_[nconf_] = fp_[ref];
-        g_[nconf_] = g_[ref];
-        anc_[nconf_] = anc_[ref];
-        vis_[nconf_] = 0;  // saved before r: visible to every later probe
-        ++nconf_;
-      }
+      keep_saved(m);
       return true;
     }
   }
 
+  // the grid chunks of this epoch saved by probe m become confirmed refs
+  // (saved before the new origin: visible to every later probe)
+  void keep_saved(uint64_t m) {
+    if (!indexable_ || !nspec_) return;
+    uint32_t nk = 0;
+    while (nk < nspec_ && ref_vis(nconf_ + nk) <= m) ++nk;  // vis grows with k
+    if (!nk) return;
+    std::vector<uint64_t> fp(nk);
+    std::vector<uint32_t> g(nk), anc(nk);
+    d2h(c_, fp.data(), c_.c_fp.p + nconf_, nk);
+    d2h(c_, g.data(), c_.c_g.p + nconf_, nk);
+    d2h(c_, anc.data(), c_.c_anc.p + nconf_, nk);
+    sync(c_);
+    const uint32_t base = nconf_;
+    for (uint32_t k = 0; k < nk; ++k) {
+      const uint32_t ref = base + k;
+      if (dead_[ref]) continue;
+      cstart_.push_back(ref_start(ref));
+      ckey_.push_back(c_.h_key[k]);
+      cfp_.push_back(fp[k]);
+      cg_.push_back(g[k]);
+      canc_.push_back(anc[k]);
+    }
+    nconf_ = (uint32_t)cstart_.size();
+  }
+
   // ---------------------------------------------------------------- finalize
   void finalize() {
+    auto t0 = Clock::now();
+    struct Done {
+      zc_stats& st;
+      Clock::time_point t;
+      ~Done() { st.finalize_ms += ms_since(t); }
+    } done{c_.stats, t0};
     std::vector<uint64_t> a, b;
     for (auto& pc : need_digest_) {
       a.push_back(pc.a);
@@ -863,6 +944,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HCK(hipEventCreate(&c->ev0));
     HCK(hipEventCreate(&c->ev1));
+    HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
   if (rc != ZC_OK) {
@@ -883,6 +965,7 @@ int zc_destroy(zc_ctx* c) {
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -942,6 +1025,10 @@ int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
   if (!c || (n && !d_data) || ((uintptr_t)d_data & 15)) return ZC_ERR_ARG;
   return guarded(c, [&] {
     DeviceGuard g(c->device);
+    // the stream may have just been written on the legacy default stream
+    // (e.g. torch's): order the context's stream after that work
+    HCK(hipEventRecord(c->ev_in, nullptr));
+    HCK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
     Resolver res(*c, (const uint8_t*)d_data, n);
     res.run();
     c->d_last = (const uint8_t*)d_data;

@@ -312,25 +312,27 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-constexpr int kRoundsPerTile = ZC_LSPAN / ZC_ROUND + 1;  // + warm-up round
+constexpr int kRounds = ZC_LSPAN / ZC_ROUND;  // rounds per tile (plus one warm-up round)
 
-// DMA of virtual round R (tile k = R / kRoundsPerTile, round R % kRoundsPerTile - 1)
-// into ring slot R % ZC_RING.  A round is ZC_ROUND = 128 bytes of each of the
-// wave's 64 rows; one instruction fills 8 rows (1 KiB); swizzle (row >> 1) & 7.
+// DMA of round r (-1 = the bytes before each span) of `tile` into ring slot
+// `slot`: ZC_ROUND = 128 bytes of each of the wave's 64 rows; one instruction
+// fills 8 rows (1 KiB); swizzle (row >> 1) & 7.  The per-lane part of the
+// source address is loop-invariant (lane_off); the rest is wave-uniform.
 __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
-                                            uint32_t lane, uint64_t R, uint32_t grid) {
-  const uint64_t k = R / kRoundsPerTile;
-  const int r = (int)(R % kRoundsPerTile) - 1;
-  const uint64_t tile = blockIdx.x + k * grid;
-  uint8_t* slot = ring + (R % ZC_RING) * (64 * ZC_ROUND);
+                                            uint32_t off_even, uint32_t off_odd, uint64_t tile, int r,
+                                            uint32_t slot) {
+  uint8_t* dst = ring + slot * (64 * ZC_ROUND);
+  const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN;
+  const bool stream_start = (r < 0 && tile0 == 0);
 #pragma unroll
   for (int j = 0; j < 64 * ZC_ROUND / 1024; ++j) {
-    const uint32_t row = j * (1024 / ZC_ROUND) + lane / (ZC_ROUND / 16);
-    const uint32_t p = (lane % (ZC_ROUND / 16)) ^ ((row >> 1) & 7);
-    const uint64_t span0 = tile * ZC_STILE + (uint64_t)(wave * 64 + row) * ZC_LSPAN;
-    const uint8_t* src = (r < 0 && span0 == 0) ? data + p * 16  // stream start: unused
-                                               : data + span0 + (int64_t)r * ZC_ROUND + p * 16;
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(slot + j * 1024), 16, 0, 0);
+    const uint8_t* base = data + tile0 + (uint64_t)j * (1024 / ZC_ROUND) * ZC_LSPAN + (int64_t)r * ZC_ROUND;
+    // span 0 has no bytes before it: its lanes of the warm-up round read the
+    // span itself instead (the gear of span 0 then starts from zero)
+    const uint32_t lane_off = (j & 1) ? off_odd : off_even;
+    const bool row0 = stream_start && j == 0 && lane_off < ZC_LSPAN;
+    const uint8_t* src = row0 ? data + lane_off : base + lane_off;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(dst + j * 1024), 16, 0, 0);
   }
 }
 
@@ -346,40 +348,51 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   const uint32_t grid = gridDim.x;
   uint8_t* myring = ring[wave];
   WaveList wl{wlist[wave], 0};
-  const uint64_t ntk = nfull > blockIdx.x ? (nfull - 1 - blockIdx.x) / grid + 1 : 0;
-  const uint64_t nR = ntk * kRoundsPerTile;
-  for (uint64_t R = 0; R < nR && R < ZC_RING - 1; ++R) stage_round(data, myring, wave, lane, R, grid);
+  const uint32_t ntk = nfull > blockIdx.x ? (uint32_t)((nfull - 1 - blockIdx.x) / grid + 1) : 0;
+  // this lane's share of DMA instruction j: row j * 8 + lane / 8 of the wave,
+  // piece (lane % 8) ^ ((row >> 1) & 7); the swizzle term is (lane / 16) ^ 4 * (j & 1)
+  const uint32_t drow = lane / (ZC_ROUND / 16);
+  const uint32_t dpiece = (lane % (ZC_ROUND / 16)) ^ ((drow >> 1) & 7);
+  const uint32_t off_even = drow * ZC_LSPAN + dpiece * 16;
+  const uint32_t off_odd = drow * ZC_LSPAN + (dpiece ^ 4) * 16;
+  const uint32_t sw = (lane >> 1) & 7;  // read-side swizzle of this lane's row
+  if (ntk) stage_round(data, myring, wave, off_even, off_odd, blockIdx.x, -1, 0);
+  uint32_t R = 0;  // rounds consumed (ring slot = R % 2)
 
-  ScanLane s{0, 0, 0};
-  const uint32_t sw = (lane >> 1) & 7;
 #pragma unroll 1
-  for (uint64_t R = 0; R < nR; ++R) {
-    if (R + ZC_RING - 1 < nR) {
-      stage_round(data, myring, wave, lane, R + ZC_RING - 1, grid);
-      wait_vmcnt<(64 * ZC_ROUND / 1024) * (ZC_RING - 1)>();  // round R's DMA has landed
-    } else {
-      wait_vmcnt<0>();
-    }
-    const uint64_t tile = blockIdx.x + (R / kRoundsPerTile) * grid;
-    const int r = (int)(R % kRoundsPerTile) - 1;
+  for (uint32_t k = 0; k < ntk; ++k) {
+    const uint64_t tile = blockIdx.x + (uint64_t)k * grid;
     const uint64_t span0 = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
-    const uint8_t* row = myring + (R % ZC_RING) * (64 * ZC_ROUND) + lane * ZC_ROUND;
-    if (r < 0) {
-      // new tile: fresh lane state, gear warmed with the 32 bytes before the span
-      s = ScanLane{0, 0, 0};
-      wl.n = 0;
-      if (span0 >= 64) {
+    // warm-up round: the 32 bytes before the span prime the gear
+    stage_round(data, myring, wave, off_even, off_odd, tile, 0, (R + 1) & 1);
+    wait_vmcnt<64 * ZC_ROUND / 1024>();
+    ScanLane s{0, 0, 0};
+    wl.n = 0;
+    if (span0 >= 64) {
+      const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND) + lane * ZC_ROUND;
 #pragma unroll
-        for (int p = (ZC_ROUND - 32) / 16; p < ZC_ROUND / 16; ++p) {
-          const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
-          const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+      for (int p = (ZC_ROUND - 32) / 16; p < ZC_ROUND / 16; ++p) {
+        const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
+        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
-        }
+          for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
-    } else {
+    }
+    ++R;
+#pragma unroll 1
+    for (int r = 0; r < kRounds; ++r) {
+      if (r + 1 < kRounds) {
+        stage_round(data, myring, wave, off_even, off_odd, tile, r + 1, (R + 1) & 1);
+        wait_vmcnt<64 * ZC_ROUND / 1024>();  // round r's DMA has landed
+      } else if (k + 1 < ntk) {
+        stage_round(data, myring, wave, off_even, off_odd, tile + grid, -1, (R + 1) & 1);
+        wait_vmcnt<64 * ZC_ROUND / 1024>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND) + lane * ZC_ROUND;
 #pragma unroll
       for (int p = 0; p < ZC_ROUND / 16; ++p) {
         const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
@@ -393,38 +406,36 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
         blk[(span0 + (uint64_t)r * ZC_ROUND) / ZC_SPAN] = ((uint64_t)s.hhi << 32) | s.hlo;
         s.hlo = s.hhi = 0;
       }
-      if (r == ZC_LSPAN / ZC_ROUND - 1) {
-        // end of tile: move this wave's anchors to the per-span slots
-        const uint64_t sidx = span0 / ZC_LSPAN;
-        if (wl.n > ZC_WLIST) {
-          span_anchors_rescan(data, n, span0, lo_thr, false, blk, arel, ag, acnt, ovf_list, ovf_cap,
-                              counters);
-        } else {
-          uint32_t cnt = 0;
-          for (uint32_t i = 0; i < wl.n; ++i) {
-            const uint32_t e0 = wl.e[2 * i];
-            if ((e0 >> 16) == lane) {
-              const uint32_t rl = e0 & 0xFFFFu;
-              if (span0 + rl >= ZC_ANCHOR_MIN_OFF) {
-                if (cnt < ZC_ANC_SLOTS) {
-                  arel[sidx * ZC_ANC_SLOTS + cnt] = (uint16_t)rl;
-                  ag[sidx * ZC_ANC_SLOTS + cnt] = wl.e[2 * i + 1];
-                }
-                ++cnt;
-              }
+      ++R;
+    }
+    // end of tile: move this wave's anchors to the per-span slots
+    const uint64_t sidx = span0 / ZC_LSPAN;
+    if (wl.n > ZC_WLIST) {
+      span_anchors_rescan(data, n, span0, lo_thr, false, blk, arel, ag, acnt, ovf_list, ovf_cap, counters);
+    } else {
+      uint32_t cnt = 0;
+      for (uint32_t i = 0; i < wl.n; ++i) {
+        const uint32_t e0 = wl.e[2 * i];
+        if ((e0 >> 16) == lane) {
+          const uint32_t rl = e0 & 0xFFFFu;
+          if (span0 + rl >= ZC_ANCHOR_MIN_OFF) {
+            if (cnt < ZC_ANC_SLOTS) {
+              arel[sidx * ZC_ANC_SLOTS + cnt] = (uint16_t)rl;
+              ag[sidx * ZC_ANC_SLOTS + cnt] = wl.e[2 * i + 1];
             }
+            ++cnt;
           }
-          acnt[sidx] = cnt;
-          if (cnt > ZC_ANC_SLOTS) {
-            unsigned long long k = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
-            if (k < ovf_cap) {
-              ovf_list[2 * k] = (uint32_t)sidx;
-              ovf_list[2 * k + 1] = cnt;
-            }
-          }
-          if (cnt) atomicAdd(&counters[CNT_POOL], (unsigned long long)cnt);
         }
       }
+      acnt[sidx] = cnt;
+      if (cnt > ZC_ANC_SLOTS) {
+        unsigned long long q = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+        if (q < ovf_cap) {
+          ovf_list[2 * q] = (uint32_t)sidx;
+          ovf_list[2 * q + 1] = cnt;
+        }
+      }
+      if (cnt) atomicAdd(&counters[CNT_POOL], (unsigned long long)cnt);
     }
   }
 }
@@ -481,16 +492,22 @@ __device__ __forceinline__ SpanAnchors span_anchors(const AnchorView& av, uint64
 }
 
 // ---------------------------------------------------------------------------
-// zc_chunk_meta: thread per chunk [start, start+W): key, first anchor (offset,
-// gear value, 64-byte fingerprint)
+// zc_chunk_meta: thread per grid chunk i of the epoch, start = r_e + i * W:
+// start, visibility time, key, first anchor (offset, gear value, 64-byte
+// fingerprint); the chunk is not yet consumed by a match (dead = 0)
 __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
-                                     const uint64_t* __restrict__ blk, AnchorView av,
-                                     const uint64_t* __restrict__ starts, uint32_t nchunks, uint32_t W,
-                                     uint64_t pw, uint64_t* __restrict__ key, uint32_t* __restrict__ cg,
-                                     uint64_t* __restrict__ cfp, uint32_t* __restrict__ anc_off) {
+                                     const uint64_t* __restrict__ blk, AnchorView av, uint64_t r_e,
+                                     uint32_t nchunks, uint32_t W, uint64_t pw,
+                                     uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
+                                     uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
+                                     uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
+                                     uint32_t* __restrict__ anc_off) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nchunks) return;
-  const uint64_t c = starts[i];
+  const uint64_t c = r_e + (uint64_t)i * W;
+  start[i] = c;
+  vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
+  dead[i] = 0;
   key[i] = pw + rk_acc(data, blk, c, c + W);
   uint32_t off = ZC_NO_ANCHOR, gv = 0;
   uint64_t f = 0;
@@ -518,6 +535,16 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   anc_off[i] = off;
   cg[i] = gv;
   cfp[i] = f;
+}
+
+// refs without an anchor (they go through the exact-hash screen), compacted
+__global__ void zc_anchorless_kernel(const uint32_t* __restrict__ anc_off, uint32_t nref,
+                                     uint32_t* __restrict__ list, uint32_t cap,
+                                     unsigned long long* __restrict__ counters) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nref || anc_off[i] != ZC_NO_ANCHOR) return;
+  unsigned long long k = atomicAdd(&counters[CNT_ANCLESS], 1ull);
+  if (k < cap) list[k] = i;
 }
 
 // ---------------------------------------------------------------------------
@@ -959,12 +986,21 @@ hipError_t launch_anchor_dense(const uint8_t* data, uint64_t n, int32_t anchor_l
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av,
-                             const uint64_t* starts, uint32_t nchunks, uint32_t W, uint64_t pw,
-                             uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off, hipStream_t s) {
+hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
+                             uint32_t nchunks, uint32_t W, uint64_t pw, uint64_t* start, uint64_t* vis,
+                             uint8_t* dead, uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off,
+                             hipStream_t s) {
   if (!nchunks) return hipSuccess;
-  hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(nchunks, 128)), dim3(128), 0, s, data, n,
-                     blk, av, starts, nchunks, W, pw, key, cg, cfp, anc_off);
+  hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(nchunks, 128)), dim3(128), 0, s, data, n, blk, av,
+                     r_e, nchunks, W, pw, start, vis, dead, key, cg, cfp, anc_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_anchorless(const uint32_t* anc_off, uint32_t nref, uint32_t* list, uint32_t cap,
+                             unsigned long long* counters, hipStream_t s) {
+  if (!nref) return hipSuccess;
+  hipLaunchKernelGGL(zc_anchorless_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, anc_off, nref, list,
+                     cap, counters);
   return hipGetLastError();
 }
 
