@@ -106,6 +106,18 @@ def test_random_streams_vs_oracle(torch_cuda, seed):
     assert _run_device(torch_cuda, data, W) == want, spec
 
 
+# streams of several full 2 MiB scan tiles plus a partial one: the persistent
+# scan kernel (not only the tail kernel) at every anchor rate, including the
+# dense small-W rates where a dword holds several anchors, spans overflow
+# their anchor slots and waves overflow their LDS anchor lists
+@pytest.mark.parametrize("W", [128, 257, 1000, 4096, 65536])
+def test_multi_tile_vs_oracle(torch_cuda, W):
+    spec = f"R{W}:3000000,C1000:1500000,Z:300000,B7:100000,C5:2000000,R77:411111"
+    data = oracle.gen(spec)
+    want = oracle.chunk(data, W)
+    assert _run_device(torch_cuda, data, W) == want
+
+
 def test_index_persists_across_streams(torch_cuda):
     # ChunkStorage::Writer::add -> ChunkIndex::addChunk: a second stream on the
     # same context matches the first stream's chunks (zutils.cc:137-166 reuses

@@ -29,6 +29,8 @@ int main(int argc, char** argv) {
     {"no_digest_no_record", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_RECORD>, {}},
     {"digest_only", zc_scan_kernel<ABL_NO_GEAR>, {}},
     {"stage_only", zc_scan_kernel<ABL_NO_BYTES>, {}},
+    {"stage_only_no_tile_end", zc_scan_kernel<ABL_NO_BYTES | ABL_NO_TILE_END>, {}},
+    {"full_no_tile_end", zc_scan_kernel<ABL_NO_TILE_END>, {}},
     {"gear_digest_nobranch", zc_scan_kernel<ABL_NO_BRANCH>, {}},
     {"gear_nobranch", zc_scan_kernel<ABL_NO_BRANCH | ABL_NO_DIGEST>, {}},
     {"full_never_taken", zc_scan_kernel<ABL_NEVER>, {}},

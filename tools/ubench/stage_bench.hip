@@ -59,6 +59,58 @@ __global__ void __launch_bounds__(TPB) stage_kernel(const uint8_t* __restrict__ 
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// the scan kernel's schedule: wait for round R, read the lane's row into
+// registers, refill the slot with round R + SLOTS, then "compute" (an xor per
+// dword plus EXTRA dependent VALU ops per dword, to mimic hashing work)
+template <int TPB, int ROWB, int SLOTS, int EXTRA>
+__global__ void __launch_bounds__(TPB, 1) stage2_kernel(const uint8_t* __restrict__ data, uint64_t ntiles, uint32_t* out) {
+  constexpr int RPI = 1024 / ROWB;
+  constexpr int NI = 64 / RPI;
+  constexpr int PIECES = ROWB / 16;
+  constexpr int ROUNDS = S / ROWB;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[TPB / 64][SLOTS][64 * ROWB];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t acc = 0;
+  const uint64_t ntk = ntiles > blockIdx.x ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const uint64_t nR = ntk * ROUNDS;
+  auto swz = [](uint32_t row) { return PIECES == 16 ? (row & 15) : PIECES == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3); };
+  auto issue = [&](uint64_t R) {
+    const uint64_t tile = blockIdx.x + (R / ROUNDS) * gridDim.x;
+    const uint32_t r = R % ROUNDS;
+    uint8_t* slot = ring[wave][R % SLOTS];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const uint32_t row = j * RPI + lane / PIECES;
+      const uint32_t p = (lane % PIECES) ^ swz(row);
+      const uint8_t* src = data + tile * (uint64_t)(TPB * S) + (uint64_t)(wave * 64 + row) * S + r * ROWB + p * 16;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(slot + j * 1024), 16, 0, 0);
+    }
+  };
+  for (uint64_t R = 0; R < nR && R < SLOTS; ++R) issue(R);
+  for (uint64_t R = 0; R < nR; ++R) {
+    if (R + SLOTS - 1 < nR) wait_vmcnt<NI * (SLOTS - 1)>();
+    else wait_vmcnt<0>();
+    const uint8_t* row = ring[wave][R % SLOTS] + lane * ROWB;
+    uint4 v[PIECES];
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) v[p] = *(const uint4*)(row + ((p ^ swz(lane)) << 4));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (R + SLOTS < nR) issue(R + SLOTS);
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) {
+      uint32_t xs[4] = {v[p].x, v[p].y, v[p].z, v[p].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t x = xs[d];
+#pragma unroll
+        for (int e = 0; e < EXTRA; ++e) x = (x << 1) + (x >> 3);
+        acc ^= x;
+      }
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 // per-lane register loads of the lane's own span, BATCH bytes per lane in flight x 2
 template <int TPB, int BATCH>
 __global__ void __launch_bounds__(TPB) reg_kernel(const uint8_t* __restrict__ data, uint64_t ntiles, uint32_t* out) {
@@ -102,6 +154,11 @@ int main() {
   STG(512, 64, 4, 1) STG(512, 128, 2, 1) STG(256, 128, 2, 2) STG(256, 128, 4, 1) STG(256, 256, 2, 1)
   STG(256, 64, 4, 2) STG(128, 256, 2, 2) STG(512, 64, 2, 2) STG(256, 64, 2, 4) STG(256, 128, 3, 1)
   STG(128, 128, 4, 2) STG(64, 256, 4, 4)
+#define ST2(TPB, ROWB, SLOTS, EXTRA) vs.push_back({"stage2 tpb=" #TPB " rowb=" #ROWB " slots=" #SLOTS " extra=" #EXTRA, [=] { \
+    uint64_t nt = n / (TPB * (uint64_t)S); hipLaunchKernelGGL((stage2_kernel<TPB, ROWB, SLOTS, EXTRA>), dim3(std::min<uint64_t>(nt, (uint64_t)cus)), dim3(TPB), 0, 0, d, nt, out); }, {}});
+  ST2(512, 128, 2, 0) ST2(512, 256, 1, 0) ST2(256, 256, 2, 0) ST2(512, 128, 2, 8) ST2(512, 256, 1, 8)
+  ST2(256, 256, 2, 8) ST2(512, 128, 2, 16) ST2(512, 256, 1, 16) ST2(256, 256, 2, 16)
+  ST2(512, 64, 4, 0) ST2(512, 64, 4, 8) ST2(512, 64, 4, 16)
 #define REG(TPB, BATCH, WPC) vs.push_back({"reg tpb=" #TPB " batch=" #BATCH " wg/cu=" #WPC, [=] { \
     uint64_t nt = n / (TPB * (uint64_t)S); hipLaunchKernelGGL((reg_kernel<TPB, BATCH>), dim3(std::min<uint64_t>(nt, (uint64_t)cus * WPC)), dim3(TPB), 0, 0, d, nt, out); }, {}});
   REG(256, 128, 8) REG(256, 256, 4) REG(256, 64, 8) REG(512, 128, 4)

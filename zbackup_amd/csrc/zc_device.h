@@ -20,7 +20,7 @@ constexpr int ZC_LSPAN = 4096;
 constexpr uint64_t ZC_STILE = (uint64_t)ZC_LSPAN * ZC_SCAN_TPB;
 constexpr int ZC_ROUND = 128;
 constexpr int ZC_RING = 2;
-constexpr int ZC_WLIST = 320;                                // per-wave LDS anchor list entries
+constexpr int ZC_WLIST = 144;                                // per-wave LDS list of pieces with anchors
 constexpr int ZC_ANC_SLOTS = 16;                             // anchor slots per lane span
 // zc_fscan: lane span 1 KiB, 256 KiB per workgroup
 constexpr uint64_t ZC_TILE = (uint64_t)ZC_SPAN * ZC_TPB;
@@ -43,9 +43,10 @@ inline int32_t anchor_lo_for(uint32_t W) {
 }
 
 // Anchors of the stream, per 4 KiB lane span s: cnt[s] anchors, in position
-// order; if cnt[s] <= ZC_ANC_SLOTS they sit in the fixed slots
-// rel/g[s * ZC_ANC_SLOTS ...], otherwise in the overflow pool at ovf_off[s].
-// Position = s * ZC_LSPAN + rel; g = gear value at that position.
+// order; if cnt[s] <= ZC_ANC_SLOTS they sit in the fixed slots, slot-major
+// (slot k of span s at rel/g[k * stride + s], so the first anchors of
+// consecutive spans are contiguous), otherwise in the overflow pool at
+// ovf_off[s].  Position = s * ZC_LSPAN + rel; g = gear value at that position.
 struct AnchorView {
   const uint32_t* cnt;
   const uint16_t* rel;
@@ -53,7 +54,13 @@ struct AnchorView {
   const uint64_t* ovf_off;
   const uint16_t* orel;
   const uint32_t* og;
+  uint64_t stride;  // = anchor_slot_stride(n)
 };
+
+// lane spans covered by the scan's tiles (incl. ones past the end of the stream)
+__host__ __device__ inline uint64_t anchor_slot_stride(uint64_t n) {
+  return (n + ZC_STILE - 1) / ZC_STILE * ZC_SCAN_TPB;
+}
 
 struct Run {  // maximal run [start, end) of screen hits of the F scan
   uint64_t start, end;

@@ -278,8 +278,7 @@ class Resolver {
 
   // ---------------------------------------------------------------- scan
   void scan() {
-    const uint64_t ntiles = (n_ + ZC_STILE - 1) / ZC_STILE;
-    const uint64_t nslots = ntiles * ZC_SCAN_TPB;  // lane spans, incl. ones past the end
+    const uint64_t nslots = anchor_slot_stride(n_);  // lane spans, incl. ones past the end
     nls_ = (n_ + ZC_LSPAN - 1) / ZC_LSPAN;
     const uint32_t ovf_cap = 1u << 16;
     c_.blk.ensure((n_ + ZC_SPAN - 1) / ZC_SPAN);
@@ -346,7 +345,7 @@ class Resolver {
       c_.orel.ensure(1);
       c_.og.ensure(1);
     }
-    av_ = AnchorView{c_.acnt.p, c_.arel.p, c_.ag.p, c_.ovf_off.p, c_.orel.p, c_.og.p};
+    av_ = AnchorView{c_.acnt.p, c_.arel.p, c_.ag.p, c_.ovf_off.p, c_.orel.p, c_.og.p, nslots};
   }
 
   // ---------------------------------------------------------------- epoch

@@ -177,12 +177,14 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 // 1 = no digest, 2 = no gear/anchors, 4 = anchors counted but not recorded,
 // 8 = skip the per-byte work entirely (staging + reads only),
 // 16 = gear + max computed but folded into the state without a ballot/branch,
-// 32 = anchor threshold raised so the recording block is (almost) never taken
+// 32 = anchor threshold raised so the recording block is (almost) never taken,
+// 64 = no tile-end work (span digests, anchor slots)
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32 };
+       ABL_NEVER = 32, ABL_NO_TILE_END = 64 };
 
-struct WaveList {   // per-wave LDS anchor list: {lane << 16 | rel, gear}
-  uint32_t* e;
+struct WaveList {   // per-wave LDS list of pieces holding anchors
+  uint32_t* e;      // {lane << 16 | rel of the piece, gear before the piece}
+  uint4* x;         // the piece's 16 bytes
   uint32_t n;       // wave-uniform count (may exceed capacity: then rescan)
 };
 
@@ -199,64 +201,68 @@ __device__ __forceinline__ void add64_pair(uint32_t& hlo, uint32_t& hhi, uint32_
   hhi = (uint32_t)(r >> 32);
 }
 
-// One dword (4 stream bytes) of the scan.  Gear: position k of the dword is
+// One 16-byte piece of the scan (four dwords).  Gear: position k of a dword is
 // g_k = (g << (k+1)) + sum_{j<=k} b_j 2^(k-j), the byte-weighted sums coming
 // from v_dot4_u32_u8, so the four positions are independent of each other.
 // Digest: acc*257 + b = ((acc << 8) | b) + acc, where (acc << 8) | b is one
 // v_perm_b32 (low word) and one v_alignbit_b32 (high word), then one 64-bit
-// add.  Anchor test: one compare of the dword's max gear and one ballot; the
-// recording block below is wave-uniform (the list count stays scalar) and is
-// entered in ~6 % of dwords at the 1/4096 anchor rate.
+// add.  Anchor test: one compare of the piece's max gear and one ballot per
+// piece.  The recording block is wave-uniform (the list count stays scalar)
+// and entered for ~22 % of pieces at the 1/4096 anchor rate: each lane with a
+// hit appends the piece (its bytes and the gear before it) to the wave's LDS
+// list, and the tile end re-derives the exact anchors from those 16 bytes.
 template <int ABL>
-__device__ __forceinline__ void scan_dword(uint32_t x, uint32_t rel, uint32_t lane, int32_t lo_thr,
+__device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane, int32_t lo_thr,
                                            ScanLane& s, WaveList& wl) {
+  const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
   if (ABL & ABL_NO_BYTES) {
-    s.hlo ^= x;
+    s.hlo ^= xs[0] ^ xs[1] ^ xs[2] ^ xs[3];
     return;
   }
-  uint32_t g[4];
-  if (!(ABL & ABL_NO_GEAR)) {
-    const uint32_t d[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
-                           __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
-                           __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
+  const uint32_t g0 = s.glo;  // gear before the piece
+  uint32_t g[4][4];
+  int32_t mx[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) g[k] = (s.glo << (k + 1)) + d[k];
-    s.glo = g[3];
-  }
-  if (!(ABL & ABL_NO_DIGEST)) {
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t x = xs[d];
+    if (!(ABL & ABL_NO_GEAR)) {
+      const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
+                              __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
+                              __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t slo = __builtin_amdgcn_perm(s.hlo, x, 0x06050400u | k);
-      const uint32_t shi = __builtin_amdgcn_alignbit(s.hhi, s.hlo, 24);
-      add64_pair(s.hlo, s.hhi, slo, shi);
+      for (int k = 0; k < 4; ++k) g[d][k] = (s.glo << (k + 1)) + dd[k];
+      s.glo = g[d][3];
+      mx[d] = max(max((int32_t)g[d][0], (int32_t)g[d][1]), max((int32_t)g[d][2], (int32_t)g[d][3]));
+    }
+    if (!(ABL & ABL_NO_DIGEST)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t slo = __builtin_amdgcn_perm(s.hlo, x, 0x06050400u | k);
+        const uint32_t shi = __builtin_amdgcn_alignbit(s.hhi, s.hlo, 24);
+        add64_pair(s.hlo, s.hhi, slo, shi);
+      }
     }
   }
   if (ABL & ABL_NO_GEAR) return;
-  const int32_t mx = max(max((int32_t)g[0], (int32_t)g[1]), max((int32_t)g[2], (int32_t)g[3]));
+  const int32_t m = max(max(mx[0], mx[1]), max(mx[2], mx[3]));
   if (ABL & ABL_NO_BRANCH) {
-    s.hhi ^= (uint32_t)mx;
+    s.hhi ^= (uint32_t)m;
     return;
   }
   if (ABL & ABL_NEVER) lo_thr = 0x7FFFFFFF;
-  const uint64_t any = __ballot(mx >= lo_thr);
+  const uint64_t any = __ballot(m >= lo_thr);
   if (__builtin_expect(any != 0, 0)) {
     if (ABL & ABL_NO_RECORD) {
       wl.n += __popcll(any);
       return;
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint64_t mk = __ballot((int32_t)g[k] >= lo_thr);
-      if (mk) {
-        const uint32_t idx = wl.n + lane_prefix(mk);
-        if (((mk >> lane) & 1) && idx < ZC_WLIST) {
-          uint32_t* e = wl.e + idx * 2;
-          e[0] = (lane << 16) | (rel + k);
-          e[1] = g[k];
-        }
-        wl.n += __popcll(mk);
-      }
+    const uint32_t idx = wl.n + lane_prefix(any);
+    if (m >= lo_thr && idx < ZC_WLIST) {
+      wl.e[2 * idx] = (lane << 16) | rel;
+      wl.e[2 * idx + 1] = g0;
+      wl.x[idx] = v;
     }
+    wl.n += __popcll(any);
   }
 }
 
@@ -267,7 +273,7 @@ __device__ void span_anchors_rescan(const uint8_t* __restrict__ data, uint64_t n
                                     uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
                                     uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list,
                                     uint32_t ovf_cap, unsigned long long* __restrict__ counters) {
-  const uint64_t sidx = span0 / ZC_LSPAN;
+  const uint64_t sidx = span0 / ZC_LSPAN, stride = anchor_slot_stride(n);
   ScanLane s{0, 0, 0};
   if (span0 >= 64) {
     for (uint64_t i = span0 - 64; i < span0; ++i) gear_step(data[i], s);
@@ -286,8 +292,8 @@ __device__ void span_anchors_rescan(const uint8_t* __restrict__ data, uint64_t n
     }
     if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) {
       if (cnt < ZC_ANC_SLOTS) {
-        arel[sidx * ZC_ANC_SLOTS + cnt] = (uint16_t)(p - span0);
-        ag[sidx * ZC_ANC_SLOTS + cnt] = s.glo;
+        arel[cnt * stride + sidx] = (uint16_t)(p - span0);
+        ag[cnt * stride + sidx] = s.glo;
       }
       ++cnt;
     }
@@ -313,29 +319,189 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 constexpr int kRounds = ZC_LSPAN / ZC_ROUND;  // rounds per tile (plus one warm-up round)
+constexpr int kDmaRound = 64 * ZC_ROUND / 1024;  // DMA instructions per wave-round
+constexpr int kDmaWarm = 2;                      // ... per warm-up round (64 x 32 B)
 
-// DMA of round r (-1 = the bytes before each span) of `tile` into ring slot
-// `slot`: ZC_ROUND = 128 bytes of each of the wave's 64 rows; one instruction
-// fills 8 rows (1 KiB); swizzle (row >> 1) & 7.  The per-lane part of the
-// source address is loop-invariant (lane_off); the rest is wave-uniform.
+// DMA of round r of `tile` into ring slot `slot`: ZC_ROUND = 128 bytes of each
+// of the wave's 64 rows; one instruction fills 8 rows (1 KiB); swizzle
+// (row >> 1) & 7.  The per-lane part of the source address is loop-invariant
+// (off_even / off_odd); the rest is wave-uniform.
 __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
                                             uint32_t off_even, uint32_t off_odd, uint64_t tile, int r,
                                             uint32_t slot) {
   uint8_t* dst = ring + slot * (64 * ZC_ROUND);
   const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN;
-  const bool stream_start = (r < 0 && tile0 == 0);
 #pragma unroll
-  for (int j = 0; j < 64 * ZC_ROUND / 1024; ++j) {
-    const uint8_t* base = data + tile0 + (uint64_t)j * (1024 / ZC_ROUND) * ZC_LSPAN + (int64_t)r * ZC_ROUND;
-    // span 0 has no bytes before it: its lanes of the warm-up round read the
-    // span itself instead (the gear of span 0 then starts from zero)
+  for (int j = 0; j < kDmaRound; ++j) {
+    const uint8_t* base = data + tile0 + (uint64_t)j * (1024 / ZC_ROUND) * ZC_LSPAN + (uint64_t)r * ZC_ROUND;
     const uint32_t lane_off = (j & 1) ? off_odd : off_even;
-    const bool row0 = stream_start && j == 0 && lane_off < ZC_LSPAN;
-    const uint8_t* src = row0 ? data + lane_off : base + lane_off;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + lane_off), (lds_void_t*)(dst + j * 1024), 16, 0, 0);
+  }
+}
+
+// DMA of the warm-up round of `tile`: the 32 bytes before each of the wave's
+// 64 spans (they prime the gear), row-major 32 B per row, two instructions.
+// Span 0 of the stream has no bytes before it: its lanes read the span itself
+// instead (the gear of span 0 starts from zero and ignores them).
+__device__ __forceinline__ void stage_warmup(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
+                                             uint32_t lane, uint64_t tile, uint32_t slot) {
+  uint8_t* dst = ring + slot * (64 * ZC_ROUND);
+  const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN;
+#pragma unroll
+  for (int j = 0; j < kDmaWarm; ++j) {
+    const uint64_t row = (uint64_t)j * 32 + lane / 2;
+    const uint64_t at = tile0 + row * ZC_LSPAN + (lane & 1) * 16;
+    const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
     __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(dst + j * 1024), 16, 0, 0);
   }
 }
 
+template <int N>
+__device__ __forceinline__ void wait_lgkmcnt() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n < 40 (the tile end's store count is
+// only known at run time)
+__device__ __forceinline__ void wait_vmcnt_dyn(uint32_t n) {
+  switch (n) {
+#define ZC_W(k) case k: wait_vmcnt<k>(); break;
+    ZC_W(8) ZC_W(9) ZC_W(10) ZC_W(11) ZC_W(12) ZC_W(13) ZC_W(14) ZC_W(15) ZC_W(16) ZC_W(17) ZC_W(18)
+    ZC_W(19) ZC_W(20) ZC_W(21) ZC_W(22) ZC_W(23) ZC_W(24) ZC_W(25) ZC_W(26) ZC_W(27) ZC_W(28) ZC_W(29)
+    ZC_W(30) ZC_W(31) ZC_W(32) ZC_W(33) ZC_W(34) ZC_W(35) ZC_W(36) ZC_W(37) ZC_W(38) ZC_W(39)
+#undef ZC_W
+    default: wait_vmcnt<0>();
+  }
+}
+
+// anchors of one span kept in registers at the tile end (more: slow path)
+constexpr int kTileSlots = 6;
+
+// End of a tile: the lane's four span digests, its anchors (from the wave's
+// LDS list) to the per-span slots, the wave's anchor count.  The common case
+// issues a known number of global stores and no waits, and returns that number
+// so the next round's wait can leave them in flight; the rare cases (a piece
+// with several anchors, more than kTileSlots anchors in a span, a full list,
+// the stream's first span) store directly and drain (return 0).
+__device__ __forceinline__ uint32_t scan_tile_end(const uint8_t* __restrict__ data, uint64_t n, uint64_t span0,
+                                                  uint32_t lane, int32_t lo_thr, const uint64_t (&bk)[4],
+                                                  const WaveList& wl, uint64_t* __restrict__ blk,
+                                                  uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
+                                                  uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list,
+                                                  uint32_t ovf_cap, unsigned long long* __restrict__ counters) {
+  static_assert(ZC_LSPAN / ZC_SPAN == 4, "four span digests per lane span");
+  uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
+  bo[0] = make_uint4((uint32_t)bk[0], (uint32_t)(bk[0] >> 32), (uint32_t)bk[1], (uint32_t)(bk[1] >> 32));
+  bo[1] = make_uint4((uint32_t)bk[2], (uint32_t)(bk[2] >> 32), (uint32_t)bk[3], (uint32_t)(bk[3] >> 32));
+  const uint64_t sidx = span0 / ZC_LSPAN, stride = anchor_slot_stride(n);
+  if (wl.n > ZC_WLIST) {
+    span_anchors_rescan(data, n, span0, lo_thr, false, blk, arel, ag, acnt, ovf_list, ovf_cap, counters);
+    wait_vmcnt<0>();
+    return 0;
+  }
+  // 1) lanes decode the listed pieces in parallel: hit mask (bits 0-15 of the
+  //    entry, piece index in 16-23, owner lane in 24-29) and the first hit's gear
+  for (uint32_t i = lane; i < wl.n; i += 64) {
+    const uint32_t e0 = wl.e[2 * i];
+    uint32_t g = wl.e[2 * i + 1], g1 = 0, mask = 0;
+    const uint4 v = wl.x[i];
+    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        g = (g << 1) + ((xs[d] >> (8 * k)) & 0xFFu);
+        const bool hit = (int32_t)g >= lo_thr;
+        g1 = (hit && !mask) ? g : g1;
+        mask |= hit ? 1u << (4 * d + k) : 0u;
+      }
+    wl.e[2 * i] = ((e0 >> 16) << 24) | (((e0 & 0xFFFFu) >> 4) << 16) | mask;
+    wl.e[2 * i + 1] = g1;
+  }
+  asm volatile("" ::: "memory");  // a wave's LDS accesses complete in order
+  // 2) every lane collects its own anchors, in position order, in registers
+  uint32_t cnt = 0, rr[kTileSlots], gg[kTileSlots];
+#pragma unroll
+  for (int t = 0; t < kTileSlots; ++t) rr[t] = gg[t] = 0;
+  bool slow = span0 < ZC_LSPAN;  // the stream's first span: positions < 63 are no anchors
+  for (uint32_t i = 0; i < wl.n; ++i) {
+    const uint32_t e0 = wl.e[2 * i], ge = wl.e[2 * i + 1];
+    const bool mine = (e0 >> 24) == lane;
+    const uint32_t mask = e0 & 0xFFFFu;
+    const uint32_t rel = (((e0 >> 16) & 0xFFu) << 4) + __builtin_ctz(mask | 0x10000u);
+#pragma unroll
+    for (int t = 0; t < kTileSlots; ++t) {
+      rr[t] = (mine && cnt == (uint32_t)t) ? rel : rr[t];
+      gg[t] = (mine && cnt == (uint32_t)t) ? ge : gg[t];
+    }
+    slow |= mine && (mask & (mask - 1)) != 0;
+    cnt += mine ? 1u : 0u;
+  }
+  slow |= cnt > (uint32_t)kTileSlots;
+  uint32_t nstores = 2;  // the digests
+  if (__ballot(slow)) {
+    // rare: replay this lane's pieces bytewise and store directly
+    if (slow) {
+      cnt = 0;
+      for (uint32_t i = 0; i < wl.n; ++i) {
+        const uint32_t e0 = wl.e[2 * i];
+        if ((e0 >> 24) != lane) continue;
+        const uint32_t rl = ((e0 >> 16) & 0xFFu) << 4;
+        const uint64_t q0 = span0 + rl;
+        uint32_t g = 0;
+        for (uint64_t j = q0 >= 32 ? q0 - 32 : 0; j < q0; ++j) g = (g << 1) + data[j];
+        const uint4 v = wl.x[i];
+        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t t = 0; t < 16; ++t) {
+          g = (g << 1) + ((xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+          if ((int32_t)g >= lo_thr && q0 + t >= ZC_ANCHOR_MIN_OFF) {
+            if (cnt < ZC_ANC_SLOTS) {
+              arel[cnt * stride + sidx] = (uint16_t)(rl + t);
+              ag[cnt * stride + sidx] = g;
+            }
+            ++cnt;
+          }
+        }
+      }
+      if (cnt > ZC_ANC_SLOTS) {
+        unsigned long long q = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+        if (q < ovf_cap) {
+          ovf_list[2 * q] = (uint32_t)sidx;
+          ovf_list[2 * q + 1] = cnt;
+        }
+      }
+    }
+    nstores = 0;
+  }
+  // 3) slot stores of the common case: slot t is stored by the lanes holding a
+  //    t-th anchor (one instruction pair per slot level some lane reaches)
+#pragma unroll
+  for (int t = 0; t < kTileSlots; ++t) {
+    const bool st = !slow && cnt > (uint32_t)t;
+    if (__ballot(st)) nstores += 2;
+    if (st) {
+      arel[t * stride + sidx] = (uint16_t)rr[t];
+      ag[t * stride + sidx] = gg[t];
+    }
+  }
+  acnt[sidx] = cnt;
+  // the wave's anchor count: one atomic from lane 0
+  uint32_t tot = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) tot += __shfl_xor(tot, d, 64);
+  if (lane == 0) atomicAdd(&counters[CNT_POOL], (unsigned long long)tot);
+  if (nstores == 0) {
+    wait_vmcnt<0>();
+    return 0;
+  }
+  return nstores + 2;  // + acnt + the atomic
+}
+
+// The workgroup's rounds form one flat sequence over its tiles (33 per tile:
+// the warm-up round, then 32).  A round is read from its ring slot into
+// registers first; the slot is then refilled with the round two ahead before
+// the round is hashed, so two rounds (16 KiB per wave) are in flight while a
+// wave computes.
 template <int ABL>
 __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t nfull, int32_t lo_thr,
@@ -344,11 +510,15 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     unsigned long long* __restrict__ counters) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
   __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
+  __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
+  constexpr uint32_t kRpt = kRounds + 1;  // rounds per tile, warm-up included
+  constexpr int kPieces = ZC_ROUND / 16;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t grid = gridDim.x;
   uint8_t* myring = ring[wave];
-  WaveList wl{wlist[wave], 0};
+  WaveList wl{wlist[wave], wdata[wave], 0};
   const uint32_t ntk = nfull > blockIdx.x ? (uint32_t)((nfull - 1 - blockIdx.x) / grid + 1) : 0;
+  const uint32_t nR = ntk * kRpt;
   // this lane's share of DMA instruction j: row j * 8 + lane / 8 of the wave,
   // piece (lane % 8) ^ ((row >> 1) & 7); the swizzle term is (lane / 16) ^ 4 * (j & 1)
   const uint32_t drow = lane / (ZC_ROUND / 16);
@@ -356,87 +526,66 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   const uint32_t off_even = drow * ZC_LSPAN + dpiece * 16;
   const uint32_t off_odd = drow * ZC_LSPAN + (dpiece ^ 4) * 16;
   const uint32_t sw = (lane >> 1) & 7;  // read-side swizzle of this lane's row
-  if (ntk) stage_round(data, myring, wave, off_even, off_odd, blockIdx.x, -1, 0);
-  uint32_t R = 0;  // rounds consumed (ring slot = R % 2)
+  auto issue = [&](uint32_t Rx) {
+    const uint32_t k = Rx / kRpt, r1 = Rx - k * kRpt;
+    const uint64_t tile = blockIdx.x + (uint64_t)k * grid;
+    if (r1 == 0)
+      stage_warmup(data, myring, wave, lane, tile, Rx & 1);
+    else
+      stage_round(data, myring, wave, off_even, off_odd, tile, (int)r1 - 1, Rx & 1);
+  };
+  if (nR > 0) issue(0);
+  if (nR > 1) issue(1);
+  ScanLane s{0, 0, 0};
+  uint64_t bk[4] = {0, 0, 0, 0};
+  uint64_t span0 = 0;
+  uint32_t tail_stores = 0;  // global stores the last tile end left in flight
 
 #pragma unroll 1
-  for (uint32_t k = 0; k < ntk; ++k) {
-    const uint64_t tile = blockIdx.x + (uint64_t)k * grid;
-    const uint64_t span0 = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
-    // warm-up round: the 32 bytes before the span prime the gear
-    stage_round(data, myring, wave, off_even, off_odd, tile, 0, (R + 1) & 1);
-    wait_vmcnt<64 * ZC_ROUND / 1024>();
-    ScanLane s{0, 0, 0};
-    wl.n = 0;
-    if (span0 >= 64) {
-      const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND) + lane * ZC_ROUND;
+  for (uint32_t R = 0; R < nR; ++R) {
+    const uint32_t k = R / kRpt;
+    const int r = (int)(R - k * kRpt) - 1;
+    // round R has landed once only round R + 1 (if issued) is outstanding
+    if (R + 1 >= nR) wait_vmcnt<0>();
+    else if (r == kRounds - 1) wait_vmcnt<kDmaWarm>();  // R + 1 is a warm-up round
+    else if (r < 0) wait_vmcnt_dyn(kDmaRound + tail_stores);  // the tile end's stores may stay in flight
+    else wait_vmcnt<kDmaRound>();
+    const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND);
+    if (r < 0) {
+      // warm-up round: the 32 bytes before the span prime the gear
+      const uint4 w0 = *(const uint4*)(row + lane * 32), w1 = *(const uint4*)(row + lane * 32 + 16);
+      wait_lgkmcnt<0>();  // the slot is free
+      if (R + 2 < nR) issue(R + 2);
+      span0 = (blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
+      s = ScanLane{0, 0, 0};
+      wl.n = 0;
+      if (span0 >= 64) {
+        const uint32_t xs[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-      for (int p = (ZC_ROUND - 32) / 16; p < ZC_ROUND / 16; ++p) {
-        const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
-        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
           for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
+      continue;
     }
-    ++R;
-#pragma unroll 1
-    for (int r = 0; r < kRounds; ++r) {
-      if (r + 1 < kRounds) {
-        stage_round(data, myring, wave, off_even, off_odd, tile, r + 1, (R + 1) & 1);
-        wait_vmcnt<64 * ZC_ROUND / 1024>();  // round r's DMA has landed
-      } else if (k + 1 < ntk) {
-        stage_round(data, myring, wave, off_even, off_odd, tile + grid, -1, (R + 1) & 1);
-        wait_vmcnt<64 * ZC_ROUND / 1024>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND) + lane * ZC_ROUND;
+    uint4 v[kPieces];
 #pragma unroll
-      for (int p = 0; p < ZC_ROUND / 16; ++p) {
-        const uint4 v = *(const uint4*)(row + ((p ^ sw) << 4));
-        const uint32_t rel = (uint32_t)r * ZC_ROUND + p * 16;
-        scan_dword<ABL>(v.x, rel + 0, lane, lo_thr, s, wl);
-        scan_dword<ABL>(v.y, rel + 4, lane, lo_thr, s, wl);
-        scan_dword<ABL>(v.z, rel + 8, lane, lo_thr, s, wl);
-        scan_dword<ABL>(v.w, rel + 12, lane, lo_thr, s, wl);
-      }
-      if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
-        blk[(span0 + (uint64_t)r * ZC_ROUND) / ZC_SPAN] = ((uint64_t)s.hhi << 32) | s.hlo;
-        s.hlo = s.hhi = 0;
-      }
-      ++R;
+    for (int p = 0; p < kPieces; ++p) v[p] = *(const uint4*)(row + lane * ZC_ROUND + ((p ^ sw) << 4));
+    wait_lgkmcnt<0>();  // the slot is free
+    if (R + 2 < nR) issue(R + 2);
+#pragma unroll
+    for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lane, lo_thr, s, wl);
+    if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
+      const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
+      const int q = r / (ZC_SPAN / ZC_ROUND);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (q == t) bk[t] = h;
+      s.hlo = s.hhi = 0;
     }
-    // end of tile: move this wave's anchors to the per-span slots
-    const uint64_t sidx = span0 / ZC_LSPAN;
-    if (wl.n > ZC_WLIST) {
-      span_anchors_rescan(data, n, span0, lo_thr, false, blk, arel, ag, acnt, ovf_list, ovf_cap, counters);
-    } else {
-      uint32_t cnt = 0;
-      for (uint32_t i = 0; i < wl.n; ++i) {
-        const uint32_t e0 = wl.e[2 * i];
-        if ((e0 >> 16) == lane) {
-          const uint32_t rl = e0 & 0xFFFFu;
-          if (span0 + rl >= ZC_ANCHOR_MIN_OFF) {
-            if (cnt < ZC_ANC_SLOTS) {
-              arel[sidx * ZC_ANC_SLOTS + cnt] = (uint16_t)rl;
-              ag[sidx * ZC_ANC_SLOTS + cnt] = wl.e[2 * i + 1];
-            }
-            ++cnt;
-          }
-        }
-      }
-      acnt[sidx] = cnt;
-      if (cnt > ZC_ANC_SLOTS) {
-        unsigned long long q = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
-        if (q < ovf_cap) {
-          ovf_list[2 * q] = (uint32_t)sidx;
-          ovf_list[2 * q + 1] = cnt;
-        }
-      }
-      if (cnt) atomicAdd(&counters[CNT_POOL], (unsigned long long)cnt);
-    }
+    if (r == kRounds - 1 && !(ABL & ABL_NO_TILE_END))
+      tail_stores = scan_tile_end(data, n, span0, lane, lo_thr, bk, wl, blk, arel, ag, acnt, ovf_list, ovf_cap,
+                                  counters);
   }
 }
 
@@ -477,18 +626,21 @@ __global__ void zc_anchor_dense_kernel(const uint8_t* __restrict__ data, uint64_
   }
 }
 
-// the anchors of lane span `sidx`: pointers + count
+// the anchors of lane span `sidx`: entry k at rel[k * stride], g[k * stride]
 struct SpanAnchors {
-  const uint16_t* rel;
-  const uint32_t* g;
+  const uint16_t* rel_;
+  const uint32_t* g_;
+  uint64_t stride;
   uint32_t cnt;
+  __device__ __forceinline__ uint32_t rel(uint32_t k) const { return rel_[k * stride]; }
+  __device__ __forceinline__ uint32_t g(uint32_t k) const { return g_[k * stride]; }
 };
 
 __device__ __forceinline__ SpanAnchors span_anchors(const AnchorView& av, uint64_t sidx) {
   uint32_t c = av.cnt[sidx];
-  if (c <= ZC_ANC_SLOTS) return SpanAnchors{av.rel + sidx * ZC_ANC_SLOTS, av.g + sidx * ZC_ANC_SLOTS, c};
+  if (c <= ZC_ANC_SLOTS) return SpanAnchors{av.rel + sidx, av.g + sidx, av.stride, c};
   const uint64_t o = av.ovf_off[sidx];
-  return SpanAnchors{av.orel + o, av.og + o, c};
+  return SpanAnchors{av.orel + o, av.og + o, 1, c};
 }
 
 // ---------------------------------------------------------------------------
@@ -519,13 +671,13 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
       uint32_t L = 0, R = sa.cnt;  // first entry with rel >= lo_rel
       while (L < R) {
         uint32_t mid = (L + R) >> 1;
-        if (sa.rel[mid] < lo_rel) L = mid + 1; else R = mid;
+        if (sa.rel(mid) < lo_rel) L = mid + 1; else R = mid;
       }
       if (L < sa.cnt) {
-        const uint64_t pos = sx * ZC_LSPAN + sa.rel[L];
+        const uint64_t pos = sx * ZC_LSPAN + sa.rel(L);
         if (pos <= hi) {
           off = (uint32_t)(pos - c);
-          gv = sa.g[L];
+          gv = sa.g(L);
           f = anchor_fp(data, pos);
         }
         break;  // later spans only hold later anchors
@@ -594,10 +746,10 @@ __global__ void zc_probe_kernel(const uint8_t* __restrict__ data, AnchorView av,
   SpanAnchors sa = span_anchors(av, sx);
   const uint32_t mask = (1u << tbits) - 1;
   for (uint32_t e = 0; e < sa.cnt; ++e) {
-    const uint64_t pos = sx * ZC_LSPAN + sa.rel[e];
+    const uint64_t pos = sx * ZC_LSPAN + sa.rel(e);
     if (pos < r + ZC_ANCHOR_MIN_OFF) continue;
-    const uint64_t k = sa.g[e];
-    uint32_t h = table_slot(sa.g[e], tbits);
+    const uint64_t k = sa.g(e);
+    uint32_t h = table_slot(sa.g(e), tbits);
     bool have_fp = false;
     uint64_t fp = 0;
     for (;;) {
