@@ -118,6 +118,38 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
+def _dense_anchor_pattern(W, period=16):
+    """A `period`-byte pattern whose periodic extension has an anchor in every
+    period at chunk size W (the gear of zc_device.h: sum b[q-j] 2^j mod 2^32 >=
+    anchor_lo), so wave-tiles overflow their anchor-pool share."""
+    rate = 16
+    while rate < 4096 and rate * 2 <= W // 16:
+        rate *= 2
+    lo = 0x80000000 - (1 << 32) // rate
+    rng = np.random.default_rng(77)
+    for _ in range(100000):
+        pat = rng.integers(0, 256, period, dtype=np.uint8)
+        ext = np.tile(pat, 64 // period + 2)
+        for q in range(32, 32 + period):
+            g = 0
+            for j in range(32):
+                g = (g + (int(ext[q - j]) << j)) & 0xFFFFFFFF
+            if lo <= g < 0x80000000:
+                return pat
+    raise AssertionError("no pattern found")
+
+
+@pytest.mark.parametrize("W", [4096, 65536])
+def test_dense_anchor_overflow_vs_oracle(torch_cuda, W):
+    # every period holds an anchor: ~16x the pool share per wave-tile at
+    # W = 65536, so the side-pool rescan path runs; mixed with random bytes
+    pat = _dense_anchor_pattern(W)
+    body = np.tile(pat, (3 << 20) // pat.size)
+    data = np.concatenate([oracle.gen("R9:1500000"), body, oracle.gen("R10:777777"), body[:1000003]])
+    want = oracle.chunk(data, W)
+    assert _run_device(torch_cuda, data, W) == want
+
+
 def test_index_persists_across_streams(torch_cuda):
     # ChunkStorage::Writer::add -> ChunkIndex::addChunk: a second stream on the
     # same context matches the first stream's chunks (zutils.cc:137-166 reuses

@@ -14,14 +14,15 @@ int main(int argc, char** argv) {
   uint64_t n = argc > 1 ? strtoull(argv[1], 0, 0) : (8ull << 30);
   uint8_t* d; CK(hipMalloc(&d, n));
   CK(launch_fill_splitmix64(d, n, 2024, 0));
-  uint64_t ntiles = n / ZC_STILE, nslots = ntiles * ZC_SCAN_TPB;
+  uint64_t ntiles = n / ZC_STILE, nwt = wave_tiles(n);
+  const uint32_t wcap = wave_tile_cap(65536);
   int cus = cu_count();
-  uint64_t* blk; uint16_t* arel; uint32_t* afp; uint32_t* acnt; uint32_t* ovf; unsigned long long* cnt;
-  CK(hipMalloc(&blk, n / ZC_SPAN * 8)); CK(hipMalloc(&arel, nslots * ZC_ANC_SLOTS * 2));
-  CK(hipMalloc(&afp, nslots * ZC_ANC_SLOTS * 4)); CK(hipMalloc(&acnt, nslots * 4));
-  CK(hipMalloc(&ovf, 1 << 20)); CK(hipMalloc(&cnt, 64));
+  uint64_t* blk; uint32_t *dbase, *dcnt, *prel, *pg; unsigned long long* cnt;
+  CK(hipMalloc(&blk, n / ZC_SPAN * 8)); CK(hipMalloc(&dbase, nwt * 4)); CK(hipMalloc(&dcnt, nwt * 4));
+  CK(hipMalloc(&prel, nwt * wcap * 4)); CK(hipMalloc(&pg, nwt * wcap * 4)); CK(hipMalloc(&cnt, 64));
+  const PoolOut po{dbase, dcnt, prel, pg, wcap};
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-  struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, int32_t, uint64_t*, uint16_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t, unsigned long long*); std::vector<float> t; };
+  struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
   std::vector<V> vs = {
     {"full", zc_scan_kernel<0>, {}},
     {"no_record", zc_scan_kernel<ABL_NO_RECORD>, {}},
@@ -40,7 +41,7 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
       CK(hipMemset(cnt, 0, 64));
       CK(hipEventRecord(a));
-      hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, ntiles, anchor_lo_for(65536), blk, arel, afp, acnt, ovf, 1u << 16, cnt);
+      hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, ntiles, anchor_lo_for(65536), blk, po, cnt);
       CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
       float ms; CK(hipEventElapsedTime(&ms, a, b));
       if (round) v.t.push_back(ms);

@@ -21,7 +21,10 @@ constexpr uint64_t ZC_STILE = (uint64_t)ZC_LSPAN * ZC_SCAN_TPB;
 constexpr int ZC_ROUND = 128;
 constexpr int ZC_RING = 2;
 constexpr int ZC_WLIST = 144;                                // per-wave LDS list of pieces with anchors
-constexpr int ZC_ANC_SLOTS = 16;                             // anchor slots per lane span
+// wave-tile: the 64 lane spans (256 KiB) one scan wave covers per tile;
+// wave-tile t holds stream positions [t << ZC_WT_SHIFT, (t + 1) << ZC_WT_SHIFT)
+constexpr int ZC_WT_SHIFT = 18;
+static_assert((64ull * ZC_LSPAN) == (1ull << ZC_WT_SHIFT), "wave-tile = 64 lane spans");
 // zc_fscan: lane span 1 KiB, 256 KiB per workgroup
 constexpr uint64_t ZC_TILE = (uint64_t)ZC_SPAN * ZC_TPB;
 constexpr int ZC_RUN_SLOTS = 4;                              // LDS screen-run slots per lane
@@ -36,31 +39,43 @@ constexpr int ZC_RUN_SLOTS = 4;                              // LDS screen-run s
 constexpr uint32_t ZC_ANCHOR_MIN_OFF = 63;
 constexpr uint32_t ZC_NO_ANCHOR = 0xFFFFFFFFu;
 
-inline int32_t anchor_lo_for(uint32_t W) {
+inline uint32_t anchor_rate_inv(uint32_t W) {
   uint32_t rate_inv = 16;
   while (rate_inv < 4096 && rate_inv * 2 <= W / 16) rate_inv *= 2;
-  return (int32_t)(0x80000000u - (uint32_t)(0x100000000ull / rate_inv));
+  return rate_inv;
+}
+inline int32_t anchor_lo_for(uint32_t W) {
+  return (int32_t)(0x80000000u - (uint32_t)(0x100000000ull / anchor_rate_inv(W)));
 }
 
-// Anchors of the stream, per 4 KiB lane span s: cnt[s] anchors, in position
-// order; if cnt[s] <= ZC_ANC_SLOTS they sit in the fixed slots, slot-major
-// (slot k of span s at rel/g[k * stride + s], so the first anchors of
-// consecutive spans are contiguous), otherwise in the overflow pool at
-// ovf_off[s].  Position = s * ZC_LSPAN + rel; g = gear value at that position.
+// Anchors of the stream, per wave-tile t: cnt[t] anchors, sorted by position,
+// at index base[t] of the pool (rel = position - (t << ZC_WT_SHIFT), g = gear
+// value there); base bit 31 set = the entries sit in the side pool (wave-tiles
+// whose anchors overflowed their pool share, rescanned exactly).
+// The scan gives wave-tile t the pool share [t * wcap, (t + 1) * wcap).
 struct AnchorView {
+  const uint32_t* base;
   const uint32_t* cnt;
-  const uint16_t* rel;
+  const uint32_t* rel;
   const uint32_t* g;
-  const uint64_t* ovf_off;
-  const uint16_t* orel;
-  const uint32_t* og;
-  uint64_t stride;  // = anchor_slot_stride(n)
+  const uint32_t* srel;
+  const uint32_t* sg;
 };
+constexpr uint32_t ZC_SIDE_POOL = 0x80000000u;
 
-// lane spans covered by the scan's tiles (incl. ones past the end of the stream)
-__host__ __device__ inline uint64_t anchor_slot_stride(uint64_t n) {
-  return (n + ZC_STILE - 1) / ZC_STILE * ZC_SCAN_TPB;
-}
+// wave-tiles covered by the scan's 2 MiB tiles (incl. ones past the end)
+inline uint64_t wave_tiles(uint64_t n) { return (n + ZC_STILE - 1) / ZC_STILE * (ZC_SCAN_TPB / 64); }
+// pool share per wave-tile: twice the expected anchor count plus slack
+inline uint32_t wave_tile_cap(uint32_t W) { return 2u * ((1u << ZC_WT_SHIFT) / anchor_rate_inv(W)) + 64u; }
+
+// where the scan writes anchors
+struct PoolOut {
+  uint32_t* base;
+  uint32_t* cnt;
+  uint32_t* rel;
+  uint32_t* g;
+  uint32_t wcap;
+};
 
 struct Run {  // maximal run [start, end) of screen hits of the F scan
   uint64_t start, end;
@@ -73,22 +88,22 @@ struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
 };
 
 // Counters word layout (uint64 each)
-// CNT_POOL: anchors found; CNT_OVERFLOW: lane spans over ZC_ANC_SLOTS anchors;
-// CNT_FOVF: screen-run buffer overflow flag
-// CNT_ANCLESS: refs without an anchor
-enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_ANCLESS = 5, CNT_LAST = 8 };
+// CNT_POOL: anchors found; CNT_OVERFLOW: wave-tiles over their pool share;
+// CNT_FOVF: screen-run buffer overflow flag; CNT_ANCLESS: class leaders
+// without an anchor; CNT_CLASS: refs that are not the leader of their class
+enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_ANCLESS = 5, CNT_CLASS = 6,
+       CNT_LAST = 8 };
 
 // --- launchers (return hipError_t of the launch) ---------------------------
-hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, uint16_t* arel,
-                       uint32_t* ag, uint32_t* acnt, uint32_t* ovf_list, uint32_t ovf_cap,
+hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s);
 
-// ovf_list holds (span, count) pairs of lane spans with more than
-// ZC_ANC_SLOTS anchors; the dense kernel writes ovf_off[span] = offs[i] and
-// the span's anchors at that offset of the overflow pool
-hipError_t launch_anchor_dense(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* spans,
-                               uint32_t nspans, const uint64_t* offs, uint64_t* ovf_off, uint16_t* orel,
-                               uint32_t* og, hipStream_t s);
+// exact rescan of the wave-tiles the scan marked overflowed (directory count
+// 0xFFFFFFFF): pass 0 sets cnt[tiles[i]] to the exact count; pass 1 writes the
+// anchors to the side pool at sbase[i] and points base[] there
+hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* tiles,
+                                const uint32_t* sbase, uint32_t ntiles, int pass, uint32_t* base, uint32_t* cnt,
+                                uint32_t* srel, uint32_t* sg, hipStream_t s);
 
 // grid chunks i < nchunks of an epoch starting at r_e (start = r_e + i * W)
 hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
@@ -96,18 +111,26 @@ hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* bl
                              uint8_t* dead, uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off,
                              hipStream_t s);
 
-hipError_t launch_anchorless(const uint32_t* anc_off, uint32_t nref, uint32_t* list, uint32_t cap,
-                             unsigned long long* counters, hipStream_t s);
+hipError_t launch_anchorless(const uint32_t* anc_off, const uint32_t* cls, uint32_t nref, uint32_t* list,
+                             uint32_t cap, unsigned long long* counters, hipStream_t s);
+
+// content classes of refs [0, nref): cls[i] = lowest ref with an equal key and
+// equal bytes (counters[CNT_CLASS] += refs that are not leaders); the class
+// table has 2^cbits >= 2 nref slots
+hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64_t* start, uint32_t nref, uint32_t W,
+                          uint64_t* ckeys, uint32_t* cvals, uint32_t cbits, uint32_t* cls,
+                          unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s);
 hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,
-                               const uint32_t* cg, const uint32_t* anc_off, uint32_t nrefs,
+                               const uint32_t* cg, const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs,
                                hipStream_t s);
 
-hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nspans, const uint64_t* tkeys,
-                        const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp, const uint64_t* vis, const uint8_t* dead,
-                        uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
-                        unsigned long long* counters, hipStream_t s);
+// one wave per wave-tile: every anchor of the stream probes the table
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tkeys,
+                        const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp,
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t n, uint32_t W, Cand* cand,
+                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,

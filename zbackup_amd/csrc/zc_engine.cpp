@@ -147,15 +147,15 @@ struct zc_ctx {
   // scratch
   DevBuf<uint64_t> blk, ftile_off;
   DevBuf<uint32_t> ftile_cnt;
-  DevBuf<uint16_t> arel, orel;
-  DevBuf<uint32_t> ag, og;
-  DevBuf<uint64_t> ovf_off;
-  DevBuf<uint32_t> acnt, ovf_list;
+  DevBuf<uint32_t> dbase, dcnt;      // anchor directory per wave-tile
+  DevBuf<uint32_t> prel, pg, srel, sg;  // anchor pool and side pool
+  DevBuf<uint32_t> otiles, obase;
   DevBuf<unsigned long long> counters;
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
   DevBuf<uint32_t> c_anc, c_g;
   DevBuf<uint8_t> c_dead;
-  DevBuf<uint64_t> tkeys;
+  DevBuf<uint64_t> tkeys, ckeys;
+  DevBuf<uint32_t> cvals, c_cls;
   DevBuf<uint32_t> tvals;
   DevBuf<Cand> cand;
   DevBuf<uint64_t> va, vb, dout;
@@ -225,7 +225,7 @@ class Resolver {
   const uint32_t W_;
   const bool indexable_;
   uint64_t npool_ = 0;
-  uint64_t nls_ = 0;  // lane spans of the stream
+  uint64_t nwt_ = 0;  // wave-tiles of the stream
   const int32_t anchor_lo_ = anchor_lo_for(W_);
   AnchorView av_{};
 
@@ -247,6 +247,40 @@ class Resolver {
   }
   uint64_t ref_vis(uint32_t ref) const { return ref < nconf_ ? 0 : ref_start(ref) + 2ull * W_ - 1; }
   uint64_t ref_key(uint32_t ref) const { return ref < nconf_ ? ckey_[ref] : c_.h_key[ref - nconf_]; }
+
+  // content classes of this epoch as linked lists in ascending ref order (so
+  // in start and visibility order): cls_[r] = leader, cnext_[r] = next member,
+  // ccur_[leader] = first member not consumed.  Empty: every ref leads its
+  // own class.
+  static constexpr uint32_t kNone = 0xFFFFFFFFu;
+  std::vector<uint32_t> cls_, cnext_, ccur_;
+
+  void load_classes() {
+    cls_.resize(nref_);
+    d2h(c_, cls_.data(), c_.c_cls.p, nref_);
+    sync(c_);
+    cnext_.assign(nref_, kNone);
+    ccur_.resize(nref_);
+    std::vector<uint32_t> tail(nref_);
+    for (uint32_t r = 0; r < nref_; ++r) {
+      ccur_[r] = r;
+      tail[r] = r;
+      const uint32_t l = cls_[r];
+      if (l != r) {
+        cnext_[tail[l]] = r;
+        tail[l] = r;
+      }
+    }
+  }
+
+  // is some ref of the class led by `lead` in the index at probe p (cut by
+  // then and not consumed by a same-grid match)?
+  bool class_alive_visible(uint32_t lead, uint64_t p) {
+    if (cls_.empty()) return ref_vis(lead) <= p && !dead_[lead];
+    uint32_t& c = ccur_[lead];
+    while (c != kNone && dead_[c]) c = cnext_[c];
+    return c != kNone && ref_vis(c) <= p;
+  }
 
   std::unordered_map<uint64_t, std::vector<uint32_t>> fmap_;  // key -> anchorless refs (start order)
   std::unordered_map<uint64_t, std::vector<uint32_t>> smap_;  // key -> statics
@@ -278,74 +312,64 @@ class Resolver {
 
   // ---------------------------------------------------------------- scan
   void scan() {
-    const uint64_t nslots = anchor_slot_stride(n_);  // lane spans, incl. ones past the end
-    nls_ = (n_ + ZC_LSPAN - 1) / ZC_LSPAN;
-    const uint32_t ovf_cap = 1u << 16;
+    nwt_ = wave_tiles(n_);
+    const uint32_t wcap = wave_tile_cap(W_);
+    if (nwt_ * wcap >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "stream too large for the anchor pool"};
     c_.blk.ensure((n_ + ZC_SPAN - 1) / ZC_SPAN);
-    c_.acnt.ensure(nslots);
-    c_.arel.ensure(nslots * ZC_ANC_SLOTS);
-    c_.ag.ensure(nslots * ZC_ANC_SLOTS);
-    c_.ovf_list.ensure(2 * ovf_cap);
+    c_.dbase.ensure(nwt_);
+    c_.dcnt.ensure(nwt_);
+    c_.prel.ensure(nwt_ * wcap);
+    c_.pg.ensure(nwt_ * wcap);
     c_.counters.ensure(CNT_LAST);
+    c_.h_cnt.ensure(CNT_LAST);
     HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
     if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
-    HCK(launch_scan(d_, n_, anchor_lo_, c_.blk.p, c_.arel.p, c_.ag.p, c_.acnt.p, c_.ovf_list.p, ovf_cap,
+    HCK(launch_scan(d_, n_, anchor_lo_, c_.blk.p, PoolOut{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, wcap},
                     c_.counters.p, c_.stream));
     if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
-    unsigned long long cnt[CNT_LAST];
-    d2h(c_, cnt, c_.counters.p, CNT_LAST);
+    d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
     sync(c_);
     if (c_.flags & ZC_FLAG_TIMING) {
       float ms = 0;
       HCK(hipEventElapsedTime(&ms, c_.ev0, c_.ev1));
       c_.stats.scan_ms = ms;
     }
-    npool_ = cnt[CNT_POOL];
+    npool_ = c_.h_cnt[CNT_POOL];
     c_.stats.anchors = npool_;
-    const uint64_t novf = cnt[CNT_OVERFLOW];
-    c_.ovf_off.ensure(novf ? nls_ : 1);
-    if (novf) {
-      // lane spans with more anchors than slots: rescan them into an exactly
-      // sized overflow pool.  The scan listed them as (span, count) pairs.
-      std::vector<uint32_t> spans, counts;
-      if (novf <= ovf_cap) {
-        std::vector<uint32_t> pairs(2 * novf);
-        d2h(c_, pairs.data(), c_.ovf_list.p, 2 * novf);
-        sync(c_);
-        for (uint64_t k = 0; k < novf; ++k) {
-          spans.push_back(pairs[2 * k]);
-          counts.push_back(pairs[2 * k + 1]);
-        }
-      } else {  // list overflowed too (very dense data): read all counts
-        std::vector<uint32_t> all(nls_);
-        d2h(c_, all.data(), c_.acnt.p, nls_);
-        sync(c_);
-        for (uint64_t sx = 0; sx < nls_; ++sx)
-          if (all[sx] > ZC_ANC_SLOTS) {
-            spans.push_back((uint32_t)sx);
-            counts.push_back(all[sx]);
-          }
-      }
-      std::vector<uint64_t> offs(spans.size());
-      uint64_t total = 0;
-      for (size_t k = 0; k < spans.size(); ++k) {
-        offs[k] = total;
-        total += counts[k];
-      }
-      c_.orel.ensure(total);
-      c_.og.ensure(total);
-      c_.ovf_list.ensure(std::max<size_t>(spans.size(), 2 * ovf_cap));
-      c_.va.ensure(spans.size());
-      h2d(c_, c_.ovf_list.p, spans.data(), spans.size());
-      h2d(c_, c_.va.p, offs.data(), offs.size());
-      HCK(launch_anchor_dense(d_, n_, anchor_lo_, c_.ovf_list.p, (uint32_t)spans.size(), c_.va.p,
-                              c_.ovf_off.p, c_.orel.p, c_.og.p, c_.stream));
+    if (c_.h_cnt[CNT_OVERFLOW]) {
+      // wave-tiles whose anchors overflowed the scan's LDS list or their pool
+      // share (dense data): count them exactly, then rescan into a side pool
+      std::vector<uint32_t> cnt(nwt_), tiles, sbase;
+      d2h(c_, cnt.data(), c_.dcnt.p, nwt_);
       sync(c_);
+      for (uint64_t t = 0; t < nwt_; ++t)
+        if (cnt[t] == 0xFFFFFFFFu) tiles.push_back((uint32_t)t);
+      const uint32_t nt = (uint32_t)tiles.size();
+      c_.otiles.ensure(nt);
+      c_.obase.ensure(nt);
+      h2d(c_, c_.otiles.p, tiles.data(), nt);
+      HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, nullptr, nt, 0, c_.dbase.p, c_.dcnt.p, nullptr,
+                               nullptr, c_.stream));
+      d2h(c_, cnt.data(), c_.dcnt.p, nwt_);
+      sync(c_);
+      uint64_t total = 0;
+      for (uint32_t t : tiles) {
+        sbase.push_back((uint32_t)total);
+        total += cnt[t];
+      }
+      if (total >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "anchor side pool too large"};
+      npool_ += total;
+      c_.stats.anchors = npool_;
+      c_.srel.ensure(total);
+      c_.sg.ensure(total);
+      h2d(c_, c_.obase.p, sbase.data(), nt);
+      HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, c_.obase.p, nt, 1, c_.dbase.p, c_.dcnt.p,
+                               c_.srel.p, c_.sg.p, c_.stream));
     } else {
-      c_.orel.ensure(1);
-      c_.og.ensure(1);
+      c_.srel.ensure(1);
+      c_.sg.ensure(1);
     }
-    av_ = AnchorView{c_.acnt.p, c_.arel.p, c_.ag.p, c_.ovf_off.p, c_.orel.p, c_.og.p, nslots};
+    av_ = AnchorView{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p};
   }
 
   // ---------------------------------------------------------------- epoch
@@ -361,6 +385,7 @@ class Resolver {
     const uint32_t nsref = indexable_ ? nspec_ : 0;
     nref_ = nconf_ + nsref;
     dead_.assign(nref_, 0);
+    cls_.clear();
     acands_.clear();
     runs_.clear();
     fmap_.clear();
@@ -395,25 +420,33 @@ class Resolver {
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
       uint32_t tbits = 10;  // sized for every ref having an anchor
       while ((1u << tbits) < 2u * nref_) ++tbits;
+      // content classes: identical refs share one leader in the table
+      c_.ckeys.ensure(1u << tbits);
+      c_.cvals.ensure(1u << tbits);
+      c_.c_cls.ensure(nref_);
+      HCK(launch_classes(d_, c_.c_key.p, c_.c_start.p, nref_, W_, c_.ckeys.p, c_.cvals.p, tbits, c_.c_cls.p,
+                         c_.counters.p, c_.stream));
       if (npool_) {
         c_.tkeys.ensure(1u << tbits);
         c_.tvals.ensure(1u << tbits);
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         HCK(launch_table_clear(c_.tkeys.p, 1u << tbits, c_.stream));
-        HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_g.p, c_.c_anc.p, nref_, c_.stream));
-        HCK(launch_probe(d_, av_, nls_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
+        HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_g.p, c_.c_anc.p, c_.c_cls.p, nref_,
+                                c_.stream));
+        HCK(launch_probe(d_, av_, nwt_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
                          c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       }
-      HCK(launch_anchorless(c_.c_anc.p, nref_, c_.ancless.p, nref_, c_.counters.p, c_.stream));
+      HCK(launch_anchorless(c_.c_anc.p, c_.c_cls.p, nref_, c_.ancless.p, nref_, c_.counters.p, c_.stream));
       d2h(c_, c_.h_key.p, c_.c_key.p + nconf_, nsref);
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
       ncand = c_.h_cnt[CNT_CAND];
       nancless = c_.h_cnt[CNT_ANCLESS];
+      if (c_.h_cnt[CNT_CLASS]) load_classes();
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-        HCK(launch_probe(d_, av_, nls_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
+        HCK(launch_probe(d_, av_, nwt_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
                          c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
@@ -456,12 +489,23 @@ class Resolver {
     std::vector<Cand> hc(nc);
     d2h(c_, hc.data(), c_.cand.p, nc);
     sync(c_);
-    std::vector<uint64_t> wa(nc), ra(nc);
+    // a window that is exactly a grid chunk of this epoch in the candidate's
+    // class is already known equal (the class was byte-verified)
+    std::vector<uint64_t> wa, ra;
+    std::vector<uint64_t> idx;
+    std::vector<uint8_t> ok(nc, 1);
     for (uint64_t i = 0; i < nc; ++i) {
-      wa[i] = hc[i].p - W_ + 1;
-      ra[i] = ref_start(hc[i].ref);
+      const uint64_t ws = hc[i].p - W_ + 1;
+      if (!cls_.empty() && ws >= r_e_ && (ws - r_e_) % W_ == 0 && (ws - r_e_) / W_ < nref_ - nconf_) {
+        const uint32_t r = nconf_ + (uint32_t)((ws - r_e_) / W_);
+        if (cls_[r] == hc[i].ref) continue;
+      }
+      wa.push_back(ws);
+      ra.push_back(ref_start(hc[i].ref));
+      idx.push_back(i);
     }
-    std::vector<uint8_t> ok = verify_pairs(wa, ra, W_);
+    std::vector<uint8_t> vok = verify_pairs(wa, ra, W_);
+    for (size_t j = 0; j < idx.size(); ++j) ok[idx[j]] = vok[j];
     acands_.reserve(nc);
     for (uint64_t i = 0; i < nc; ++i)
       if (ok[i]) acands_.push_back({hc[i].p, hc[i].ref});
@@ -584,7 +628,7 @@ class Resolver {
     if (it == fmap_.end()) return -1;
     for (uint32_t ref : it->second) {
       if (ref_vis(ref) > p) break;
-      if (!dead_[ref]) return ref;
+      if (class_alive_visible(ref, p)) return ref;
     }
     return -1;
   }
@@ -666,7 +710,7 @@ class Resolver {
     if (it != fmap_.end()) {
       for (uint32_t ref : it->second) {
         if (ref_vis(ref) > p) break;
-        if (dead_[ref]) continue;
+        if (!class_alive_visible(ref, p)) continue;
         bool ok;
         if (fb_.vref[i] == (int64_t)ref) {
           ok = fb_.vok[i];
@@ -705,7 +749,6 @@ class Resolver {
   }
 
   // ---------------------------------------------------------------- walk
-  bool alive_visible(uint32_t ref, uint64_t p) const { return ref_vis(ref) <= p && !dead_[ref]; }
 
   void push(uint64_t off, uint32_t size, uint32_t kind, uint64_t rolling) {
     zc_record r;
@@ -771,7 +814,7 @@ class Resolver {
       uint32_t refa = 0;
       while (ia < acands_.size()) {
         const ACand& a = acands_[ia];
-        if (a.p >= x && alive_visible(a.ref, a.p)) {
+        if (a.p >= x && class_alive_visible(a.ref, a.p)) {
           pa = a.p;
           refa = a.ref;
           break;

@@ -266,47 +266,96 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane,
   }
 }
 
-// exact anchors of one span straight from global memory (the stream's partial
-// last tile, and waves whose LDS list overflowed): slots, count, overflow pair
-__device__ void span_anchors_rescan(const uint8_t* __restrict__ data, uint64_t n, uint64_t span0,
-                                    int32_t lo_thr, bool digest, uint64_t* __restrict__ blk,
-                                    uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
-                                    uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list,
-                                    uint32_t ovf_cap, unsigned long long* __restrict__ counters) {
-  const uint64_t sidx = span0 / ZC_LSPAN, stride = anchor_slot_stride(n);
+// 16 stream bytes at q (16-byte aligned), zero past the end of the stream
+__device__ __forceinline__ uint4 load16_clamped(const uint8_t* __restrict__ data, uint64_t n, uint64_t q) {
+  if (q + 16 <= n) return *(const uint4*)(data + q);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint64_t i = q; i < n && i < q + 16; ++i) w[(i - q) >> 2] |= (uint32_t)data[i] << (8 * ((i - q) & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// One 1 KiB sub-span [q0, min(q0 + 1024, n)) (q0 1 KiB aligned) read with
+// 16-byte loads, eight in flight: emit(pos, gear) for each anchor in order;
+// returns the sub-span's 64-bit Rabin-Karp digest (the block digest).  For
+// the partial last tile and the exact rescan of overflowed wave-tiles.
+template <class Emit>
+__device__ uint64_t subspan_pass(const uint8_t* __restrict__ data, uint64_t n, uint64_t q0, int32_t lo_thr,
+                                 Emit&& emit) {
   ScanLane s{0, 0, 0};
-  if (span0 >= 64) {
-    for (uint64_t i = span0 - 64; i < span0; ++i) gear_step(data[i], s);
+  if (q0 >= 32) {
+    const uint4 w[2] = {*(const uint4*)(data + q0 - 32), *(const uint4*)(data + q0 - 16)};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t xs[4] = {w[k].x, w[k].y, w[k].z, w[k].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gear_step((xs[d] >> (8 * j)) & 0xFFu, s);
+    }
   }
-  const uint64_t end = (span0 + ZC_LSPAN < n) ? span0 + ZC_LSPAN : n;
+  const uint64_t end = (q0 + ZC_SPAN < n) ? q0 + ZC_SPAN : n;
+  for (uint64_t c = q0; c < end; c += 128) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = load16_clamped(data, n, c + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t xs[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint64_t p = c + 16 * k + 4 * d + j;
+          if (p < end) {
+            const uint32_t b = (xs[d] >> (8 * j)) & 0xFFu;
+            gear_step(b, s);
+            digest_step(b, s);
+            if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) emit(p, s.glo);
+          }
+        }
+    }
+  }
+  return ((uint64_t)s.hhi << 32) | s.hlo;
+}
+
+// exclusive prefix sum over the 64 lanes of a wave; *total = the sum
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t* total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// A whole wave-tile by one 256-thread block, a 1 KiB sub-span per thread:
+// count, block prefix, write the anchors in position order at rel/g[base ...]
+// (at most cap of them); optionally the block digests.  Returns the total.
+__device__ uint32_t wave_tile_block(const uint8_t* __restrict__ data, uint64_t n, uint64_t wt, int32_t lo_thr,
+                                    uint64_t* __restrict__ blk, uint32_t* __restrict__ rel,
+                                    uint32_t* __restrict__ g, uint32_t base, uint32_t cap, uint32_t* s_tmp) {
+  static_assert((ZC_TPB * ZC_SPAN) == (1 << ZC_WT_SHIFT), "a block covers a wave-tile");
+  const uint64_t t0 = wt << ZC_WT_SHIFT, q0 = t0 + (uint64_t)threadIdx.x * ZC_SPAN;
   uint32_t cnt = 0;
-  for (uint64_t p = span0; p < end; ++p) {
-    uint32_t b = data[p];
-    gear_step(b, s);
-    if (digest) {
-      digest_step(b, s);
-      if ((p + 1) % ZC_SPAN == 0 || p + 1 == end) {
-        blk[p / ZC_SPAN] = ((uint64_t)s.hhi << 32) | s.hlo;
-        s.hlo = s.hhi = 0;
-      }
-    }
-    if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) {
-      if (cnt < ZC_ANC_SLOTS) {
-        arel[cnt * stride + sidx] = (uint16_t)(p - span0);
-        ag[cnt * stride + sidx] = s.glo;
-      }
-      ++cnt;
-    }
+  if (q0 < n) {
+    const uint64_t h = subspan_pass(data, n, q0, lo_thr, [&](uint64_t, uint32_t) { ++cnt; });
+    if (blk) blk[q0 / ZC_SPAN] = h;
   }
-  acnt[sidx] = cnt;
-  if (cnt > ZC_ANC_SLOTS) {
-    unsigned long long k = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
-    if (k < ovf_cap) {
-      ovf_list[2 * k] = (uint32_t)sidx;
-      ovf_list[2 * k + 1] = cnt;
-    }
+  uint32_t tot;
+  const uint32_t excl = block_excl_scan(cnt, s_tmp, tot);
+  if (cnt && excl < cap && rel) {
+    uint32_t k = excl;
+    subspan_pass(data, n, q0, lo_thr, [&](uint64_t p, uint32_t gv) {
+      if (k < cap) {
+        rel[base + k] = (uint32_t)(p - t0);
+        g[base + k] = gv;
+      }
+      ++k;
+    });
   }
-  if (cnt) atomicAdd(&counters[CNT_POOL], (unsigned long long)cnt);
+  return tot;
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -374,37 +423,53 @@ __device__ __forceinline__ void wait_vmcnt_dyn(uint32_t n) {
   }
 }
 
-// anchors of one span kept in registers at the tile end (more: slow path)
+// anchors of one span kept in registers at the tile end (more: a second pass
+// over the LDS list)
 constexpr int kTileSlots = 6;
+// directory count of a wave-tile left for the exact rescan
+constexpr uint32_t ZC_WT_OVERFLOW = 0xFFFFFFFFu;
 
-// End of a tile: the lane's four span digests, its anchors (from the wave's
-// LDS list) to the per-span slots, the wave's anchor count.  The common case
-// issues a known number of global stores and no waits, and returns that number
-// so the next round's wait can leave them in flight; the rare cases (a piece
-// with several anchors, more than kTileSlots anchors in a span, a full list,
-// the stream's first span) store directly and drain (return 0).
-__device__ __forceinline__ uint32_t scan_tile_end(const uint8_t* __restrict__ data, uint64_t n, uint64_t span0,
-                                                  uint32_t lane, int32_t lo_thr, const uint64_t (&bk)[4],
-                                                  const WaveList& wl, uint64_t* __restrict__ blk,
-                                                  uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
-                                                  uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list,
-                                                  uint32_t ovf_cap, unsigned long long* __restrict__ counters) {
+// End of a tile: the lane's four span digests; the wave's anchors, from its
+// LDS piece list, to the wave-tile's pool share in position order; the
+// directory entry and the anchor count.  The common case issues a known
+// number of global stores and no waits, and returns that number, so the next
+// round's wait can leave them in flight (an under-count is always safe).
+// Lanes with more than kTileSlots anchors store them in a second pass over
+// the list; a wave-tile whose list or pool share overflowed is marked for the
+// exact rescan (zc_anchor_rescan) and stores nothing.
+__device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
+                                                  const uint64_t (&bk)[4], const WaveList& wl,
+                                                  uint64_t* __restrict__ blk, PoolOut po,
+                                                  unsigned long long* __restrict__ counters) {
   static_assert(ZC_LSPAN / ZC_SPAN == 4, "four span digests per lane span");
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
   bo[0] = make_uint4((uint32_t)bk[0], (uint32_t)(bk[0] >> 32), (uint32_t)bk[1], (uint32_t)(bk[1] >> 32));
   bo[1] = make_uint4((uint32_t)bk[2], (uint32_t)(bk[2] >> 32), (uint32_t)bk[3], (uint32_t)(bk[3] >> 32));
-  const uint64_t sidx = span0 / ZC_LSPAN, stride = anchor_slot_stride(n);
+  const uint64_t wt = span0 >> ZC_WT_SHIFT;
+  const uint32_t base = (uint32_t)wt * po.wcap;
   if (wl.n > ZC_WLIST) {
-    span_anchors_rescan(data, n, span0, lo_thr, false, blk, arel, ag, acnt, ovf_list, ovf_cap, counters);
-    wait_vmcnt<0>();
+    if (lane == 0) {
+      po.cnt[wt] = ZC_WT_OVERFLOW;
+      atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+    }
     return 0;
   }
-  // 1) lanes decode the listed pieces in parallel: hit mask (bits 0-15 of the
-  //    entry, piece index in 16-23, owner lane in 24-29) and the first hit's gear
-  for (uint32_t i = lane; i < wl.n; i += 64) {
-    const uint32_t e0 = wl.e[2 * i];
-    uint32_t g = wl.e[2 * i + 1], g1 = 0, mask = 0;
-    const uint4 v = wl.x[i];
+  // 1) lanes decode the listed pieces in parallel (entry 64 c + lane in
+  //    register c): hit mask (bits 0-15), piece index (16-23), owner lane
+  //    (24-29) and the first hit's gear.  Kept in registers and read back with
+  //    v_readlane: an LDS store here would have to wait for the ring's DMA.
+  constexpr int kChunks = (ZC_WLIST + 63) / 64;
+  uint32_t ent[kChunks], eg[kChunks];
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const uint32_t i = 64 * c + lane;
+    uint32_t e0 = 0, g = 0, g1 = 0, mask = 0;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i < wl.n) {
+      e0 = wl.e[2 * i];
+      g = wl.e[2 * i + 1];
+      v = wl.x[i];
+    }
     const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int d = 0; d < 4; ++d)
@@ -415,86 +480,90 @@ __device__ __forceinline__ uint32_t scan_tile_end(const uint8_t* __restrict__ da
         g1 = (hit && !mask) ? g : g1;
         mask |= hit ? 1u << (4 * d + k) : 0u;
       }
-    wl.e[2 * i] = ((e0 >> 16) << 24) | (((e0 & 0xFFFFu) >> 4) << 16) | mask;
-    wl.e[2 * i + 1] = g1;
+    ent[c] = ((e0 >> 16) << 24) | (((e0 & 0xFFFFu) >> 4) << 16) | mask;
+    eg[c] = g1;
   }
-  asm volatile("" ::: "memory");  // a wave's LDS accesses complete in order
   // 2) every lane collects its own anchors, in position order, in registers
+  //    (offsets below 63 of the stream are no anchors)
   uint32_t cnt = 0, rr[kTileSlots], gg[kTileSlots];
 #pragma unroll
   for (int t = 0; t < kTileSlots; ++t) rr[t] = gg[t] = 0;
-  bool slow = span0 < ZC_LSPAN;  // the stream's first span: positions < 63 are no anchors
-  for (uint32_t i = 0; i < wl.n; ++i) {
-    const uint32_t e0 = wl.e[2 * i], ge = wl.e[2 * i + 1];
-    const bool mine = (e0 >> 24) == lane;
-    const uint32_t mask = e0 & 0xFFFFu;
-    const uint32_t rel = (((e0 >> 16) & 0xFFu) << 4) + __builtin_ctz(mask | 0x10000u);
+  auto push = [&](bool mine, uint32_t rel, uint32_t g) {
+    mine = mine && span0 + rel >= ZC_ANCHOR_MIN_OFF;
 #pragma unroll
     for (int t = 0; t < kTileSlots; ++t) {
       rr[t] = (mine && cnt == (uint32_t)t) ? rel : rr[t];
-      gg[t] = (mine && cnt == (uint32_t)t) ? ge : gg[t];
+      gg[t] = (mine && cnt == (uint32_t)t) ? g : gg[t];
     }
-    slow |= mine && (mask & (mask - 1)) != 0;
     cnt += mine ? 1u : 0u;
-  }
-  slow |= cnt > (uint32_t)kTileSlots;
-  uint32_t nstores = 2;  // the digests
-  if (__ballot(slow)) {
-    // rare: replay this lane's pieces bytewise and store directly
-    if (slow) {
-      cnt = 0;
-      for (uint32_t i = 0; i < wl.n; ++i) {
-        const uint32_t e0 = wl.e[2 * i];
-        if ((e0 >> 24) != lane) continue;
-        const uint32_t rl = ((e0 >> 16) & 0xFFu) << 4;
-        const uint64_t q0 = span0 + rl;
-        uint32_t g = 0;
-        for (uint64_t j = q0 >= 32 ? q0 - 32 : 0; j < q0; ++j) g = (g << 1) + data[j];
-        const uint4 v = wl.x[i];
-        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-        for (uint32_t t = 0; t < 16; ++t) {
-          g = (g << 1) + ((xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
-          if ((int32_t)g >= lo_thr && q0 + t >= ZC_ANCHOR_MIN_OFF) {
-            if (cnt < ZC_ANC_SLOTS) {
-              arel[cnt * stride + sidx] = (uint16_t)(rl + t);
-              ag[cnt * stride + sidx] = g;
-            }
-            ++cnt;
-          }
-        }
-      }
-      if (cnt > ZC_ANC_SLOTS) {
-        unsigned long long q = atomicAdd(&counters[CNT_OVERFLOW], 1ull);
-        if (q < ovf_cap) {
-          ovf_list[2 * q] = (uint32_t)sidx;
-          ovf_list[2 * q + 1] = cnt;
-        }
+  };
+  // the further anchors of a piece (rare), the gear rolled on from the first
+  auto more = [&](uint32_t i, bool mine, uint32_t mask, uint32_t p16, uint32_t t1, uint32_t g1, auto&& sink) {
+    const uint4 v = wl.x[i];
+    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+    uint32_t g = g1;
+    for (uint32_t t = t1 + 1; t < 16; ++t) {
+      g = (g << 1) + ((xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+      sink(mine && ((mask >> t) & 1), p16 + t, g);
+    }
+  };
+  // every listed entry in order: sink(...) for its anchors owned by `who`
+  auto walk = [&](bool who, auto&& sink) {
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const uint32_t m = wl.n > 64u * c ? min(wl.n - 64u * c, 64u) : 0u;
+      for (uint32_t l = 0; l < m; ++l) {
+        const uint32_t e0 = __builtin_amdgcn_readlane(ent[c], l), g1 = __builtin_amdgcn_readlane(eg[c], l);
+        const bool mine = who && (e0 >> 24) == lane;
+        const uint32_t mask = e0 & 0xFFFFu, p16 = ((e0 >> 16) & 0xFFu) << 4;
+        const uint32_t t1 = __builtin_ctz(mask | 0x10000u);
+        sink(mine, p16 + t1, g1);
+        const bool multi = mine && (mask & (mask - 1)) != 0;
+        if (__ballot(multi)) more(64 * c + l, multi, mask, p16, t1, g1, sink);
       }
     }
-    nstores = 0;
+  };
+  walk(true, push);
+  uint32_t tot;
+  const uint32_t excl = wave_excl_scan(cnt, lane, &tot);
+  if (tot > po.wcap) {
+    if (lane == 0) {
+      po.cnt[wt] = ZC_WT_OVERFLOW;
+      atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+    }
+    return 0;
   }
-  // 3) slot stores of the common case: slot t is stored by the lanes holding a
-  //    t-th anchor (one instruction pair per slot level some lane reaches)
+  const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
+  const bool slow = cnt > (uint32_t)kTileSlots;
+  uint32_t nstores = 2;  // the digests
+  // 3) the common case's pool stores: one instruction pair per slot level
+  //    some lane reaches
 #pragma unroll
   for (int t = 0; t < kTileSlots; ++t) {
     const bool st = !slow && cnt > (uint32_t)t;
     if (__ballot(st)) nstores += 2;
     if (st) {
-      arel[t * stride + sidx] = (uint16_t)rr[t];
-      ag[t * stride + sidx] = gg[t];
+      po.rel[base + excl + t] = rbase + rr[t];
+      po.g[base + excl + t] = gg[t];
     }
   }
-  acnt[sidx] = cnt;
-  // the wave's anchor count: one atomic from lane 0
-  uint32_t tot = cnt;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) tot += __shfl_xor(tot, d, 64);
-  if (lane == 0) atomicAdd(&counters[CNT_POOL], (unsigned long long)tot);
-  if (nstores == 0) {
-    wait_vmcnt<0>();
-    return 0;
+  if (__ballot(slow)) {
+    // lanes with many anchors: a second pass over the list, storing directly
+    uint32_t k = base + excl;
+    walk(slow, [&](bool mine, uint32_t rel, uint32_t g) {
+      if (mine && span0 + rel >= ZC_ANCHOR_MIN_OFF) {
+        po.rel[k] = rbase + rel;
+        po.g[k] = g;
+        ++k;
+      }
+    });
   }
-  return nstores + 2;  // + acnt + the atomic
+  if (lane == 0) {
+    po.base[wt] = base;
+    po.cnt[wt] = tot;
+    atomicAdd(&counters[CNT_POOL], (unsigned long long)tot);
+  }
+  return nstores + 3;  // + the directory pair and the anchor count
 }
 
 // The workgroup's rounds form one flat sequence over its tiles (33 per tile:
@@ -505,9 +574,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(const uint8_t* __restrict__ da
 template <int ABL>
 __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t nfull, int32_t lo_thr,
-    uint64_t* __restrict__ blk, uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
-    uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list, uint32_t ovf_cap,
-    unsigned long long* __restrict__ counters) {
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
   __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
   __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
@@ -584,63 +651,62 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       s.hlo = s.hhi = 0;
     }
     if (r == kRounds - 1 && !(ABL & ABL_NO_TILE_END))
-      tail_stores = scan_tile_end(data, n, span0, lane, lo_thr, bk, wl, blk, arel, ag, acnt, ovf_list, ovf_cap,
-                                  counters);
+      tail_stores = scan_tile_end(span0, lane, lo_thr, bk, wl, blk, po, counters);
   }
 }
 
-// the stream's last, partial tile: bytewise, one lane per span
-__global__ void __launch_bounds__(ZC_SCAN_TPB) zc_scan_tail_kernel(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile, int32_t lo_thr,
-    uint64_t* __restrict__ blk, uint16_t* __restrict__ arel, uint32_t* __restrict__ ag,
-    uint32_t* __restrict__ acnt, uint32_t* __restrict__ ovf_list, uint32_t ovf_cap,
-    unsigned long long* __restrict__ counters) {
-  const uint64_t span0 = tile * ZC_STILE + (uint64_t)threadIdx.x * ZC_LSPAN;
-  if (span0 >= n) return;
-  span_anchors_rescan(data, n, span0, lo_thr, true, blk, arel, ag, acnt, ovf_list, ovf_cap, counters);
-}
-
-// rescan of lane spans whose anchors overflowed their slots: every anchor is
-// written, in order, to the overflow pool at offs[i]; ovf_off[span] = offs[i]
-__global__ void zc_anchor_dense_kernel(const uint8_t* __restrict__ data, uint64_t n, int32_t lo_thr,
-                                       const uint32_t* __restrict__ spans, uint32_t nspans,
-                                       const uint64_t* __restrict__ offs, uint64_t* __restrict__ ovf_off,
-                                       uint16_t* __restrict__ orel, uint32_t* __restrict__ og) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nspans) return;
-  const uint64_t sidx = spans[i];
-  const uint64_t span0 = sidx * ZC_LSPAN;
-  ScanLane s{0, 0, 0};
-  if (span0 >= 64)
-    for (uint64_t q = span0 - 64; q < span0; ++q) gear_step(data[q], s);
-  const uint64_t end = (span0 + ZC_LSPAN < n) ? span0 + ZC_LSPAN : n;
-  uint64_t w = offs[i];
-  ovf_off[sidx] = w;
-  for (uint64_t p = span0; p < end; ++p) {
-    gear_step(data[p], s);
-    if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) {
-      orel[w] = (uint16_t)(p - span0);
-      og[w] = s.glo;
-      ++w;
+// the stream's last, partial tile: one 256-thread block per wave-tile, a
+// 1 KiB sub-span per thread (block digests and anchors)
+__global__ void __launch_bounds__(ZC_TPB) zc_scan_tail_kernel(const uint8_t* __restrict__ data, uint64_t n,
+                                                             uint64_t tile, int32_t lo_thr,
+                                                             uint64_t* __restrict__ blk, PoolOut po,
+                                                             unsigned long long* __restrict__ counters) {
+  __shared__ uint32_t s_tmp[ZC_TPB / 64];
+  const uint64_t wt = tile * (ZC_SCAN_TPB / 64) + blockIdx.x;
+  const uint32_t base = (uint32_t)wt * po.wcap;
+  const uint32_t tot = wave_tile_block(data, n, wt, lo_thr, blk, po.rel, po.g, base, po.wcap, s_tmp);
+  if (threadIdx.x == 0) {
+    po.base[wt] = base;
+    if (tot > po.wcap) {
+      po.cnt[wt] = ZC_WT_OVERFLOW;
+      atomicAdd(&counters[CNT_OVERFLOW], 1ull);
+    } else {
+      po.cnt[wt] = tot;
+      if (tot) atomicAdd(&counters[CNT_POOL], (unsigned long long)tot);
     }
   }
 }
 
-// the anchors of lane span `sidx`: entry k at rel[k * stride], g[k * stride]
-struct SpanAnchors {
-  const uint16_t* rel_;
-  const uint32_t* g_;
-  uint64_t stride;
+// Exact rescan of the wave-tiles marked overflowed, one block each: pass 0
+// counts (cnt[wt] = exact count), pass 1 writes the anchors into the side
+// pool at sbase[i] and points the directory there.
+__global__ void __launch_bounds__(ZC_TPB) zc_anchor_rescan_kernel(const uint8_t* __restrict__ data, uint64_t n,
+                                                                 int32_t lo_thr, const uint32_t* __restrict__ tiles,
+                                                                 const uint32_t* __restrict__ sbase, int pass,
+                                                                 uint32_t* __restrict__ dbase,
+                                                                 uint32_t* __restrict__ dcnt,
+                                                                 uint32_t* __restrict__ srel, uint32_t* __restrict__ sg) {
+  __shared__ uint32_t s_tmp[ZC_TPB / 64];
+  const uint64_t wt = tiles[blockIdx.x];
+  const uint32_t b = pass ? sbase[blockIdx.x] : 0u;
+  const uint32_t tot = wave_tile_block(data, n, wt, lo_thr, nullptr, pass ? srel : nullptr, sg, b, ~0u, s_tmp);
+  if (threadIdx.x == 0) {
+    dcnt[wt] = tot;
+    if (pass) dbase[wt] = b | ZC_SIDE_POOL;
+  }
+}
+
+// the anchors of wave-tile wt: entry k at rel[k], g[k], sorted by position
+struct TileAnchors {
+  const uint32_t* rel;
+  const uint32_t* g;
   uint32_t cnt;
-  __device__ __forceinline__ uint32_t rel(uint32_t k) const { return rel_[k * stride]; }
-  __device__ __forceinline__ uint32_t g(uint32_t k) const { return g_[k * stride]; }
 };
 
-__device__ __forceinline__ SpanAnchors span_anchors(const AnchorView& av, uint64_t sidx) {
-  uint32_t c = av.cnt[sidx];
-  if (c <= ZC_ANC_SLOTS) return SpanAnchors{av.rel + sidx, av.g + sidx, av.stride, c};
-  const uint64_t o = av.ovf_off[sidx];
-  return SpanAnchors{av.orel + o, av.og + o, 1, c};
+__device__ __forceinline__ TileAnchors tile_anchors(const AnchorView& av, uint64_t wt) {
+  const uint32_t b = av.base[wt], c = av.cnt[wt];
+  if (b & ZC_SIDE_POOL) return TileAnchors{av.srel + (b & ~ZC_SIDE_POOL), av.sg + (b & ~ZC_SIDE_POOL), c};
+  return TileAnchors{av.rel + b, av.g + b, c};
 }
 
 // ---------------------------------------------------------------------------
@@ -665,22 +731,23 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   uint64_t f = 0;
   if (W > ZC_ANCHOR_MIN_OFF) {
     const uint64_t lo = c + ZC_ANCHOR_MIN_OFF, hi = c + W - 1;  // inclusive
-    for (uint64_t sx = lo / ZC_LSPAN; sx <= hi / ZC_LSPAN; ++sx) {
-      SpanAnchors sa = span_anchors(av, sx);
-      const uint32_t lo_rel = (sx == lo / ZC_LSPAN) ? (uint32_t)(lo - sx * ZC_LSPAN) : 0;
-      uint32_t L = 0, R = sa.cnt;  // first entry with rel >= lo_rel
+    for (uint64_t wt = lo >> ZC_WT_SHIFT; wt <= (hi >> ZC_WT_SHIFT); ++wt) {
+      const TileAnchors ta = tile_anchors(av, wt);
+      const uint64_t t0 = wt << ZC_WT_SHIFT;
+      const uint32_t lo_rel = lo > t0 ? (uint32_t)(lo - t0) : 0u;
+      uint32_t L = 0, R = ta.cnt;  // first entry with rel >= lo_rel
       while (L < R) {
-        uint32_t mid = (L + R) >> 1;
-        if (sa.rel(mid) < lo_rel) L = mid + 1; else R = mid;
+        const uint32_t mid = (L + R) >> 1;
+        if (ta.rel[mid] < lo_rel) L = mid + 1; else R = mid;
       }
-      if (L < sa.cnt) {
-        const uint64_t pos = sx * ZC_LSPAN + sa.rel(L);
+      if (L < ta.cnt) {
+        const uint64_t pos = t0 + ta.rel[L];
         if (pos <= hi) {
           off = (uint32_t)(pos - c);
-          gv = sa.g(L);
+          gv = ta.g[L];
           f = anchor_fp(data, pos);
         }
-        break;  // later spans only hold later anchors
+        break;  // later wave-tiles only hold later anchors
       }
     }
   }
@@ -689,12 +756,12 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   cfp[i] = f;
 }
 
-// refs without an anchor (they go through the exact-hash screen), compacted
-__global__ void zc_anchorless_kernel(const uint32_t* __restrict__ anc_off, uint32_t nref,
-                                     uint32_t* __restrict__ list, uint32_t cap,
+// class leaders without an anchor (they go through the exact-hash screen), compacted
+__global__ void zc_anchorless_kernel(const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
+                                     uint32_t nref, uint32_t* __restrict__ list, uint32_t cap,
                                      unsigned long long* __restrict__ counters) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nref || anc_off[i] != ZC_NO_ANCHOR) return;
+  if (i >= nref || anc_off[i] != ZC_NO_ANCHOR || cls[i] != i) return;
   unsigned long long k = atomicAdd(&counters[CNT_ANCLESS], 1ull);
   if (k < cap) list[k] = i;
 }
@@ -715,9 +782,10 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
 
 __global__ void zc_table_insert_kernel(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,
                                        const uint32_t* __restrict__ cg,
-                                       const uint32_t* __restrict__ anc_off, uint32_t nrefs) {
+                                       const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
+                                       uint32_t nrefs) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrefs || anc_off[i] == ZC_NO_ANCHOR) return;
+  if (i >= nrefs || anc_off[i] == ZC_NO_ANCHOR || cls[i] != i) return;
   const uint64_t k = cg[i];
   const uint32_t mask = (1u << tbits) - 1;
   uint32_t h = table_slot(cg[i], tbits);
@@ -733,40 +801,45 @@ __global__ void zc_table_insert_kernel(uint64_t* tkeys, uint32_t* tvals, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// zc_probe: thread per lane span; every anchor probes the table
-__global__ void zc_probe_kernel(const uint8_t* __restrict__ data, AnchorView av, uint64_t nspans,
-                                const uint64_t* __restrict__ tkeys, const uint32_t* __restrict__ tvals,
-                                uint32_t tbits, const uint32_t* __restrict__ anc_off,
-                                const uint64_t* __restrict__ cfp, const uint64_t* __restrict__ vis,
-                                const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W,
-                                Cand* __restrict__ cand, uint64_t cand_cap,
-                                unsigned long long* __restrict__ counters) {
-  uint64_t sx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sx >= nspans) return;
-  SpanAnchors sa = span_anchors(av, sx);
+// zc_probe: one wave per wave-tile, a lane per anchor; every anchor probes the
+// table (key = gear value, confirmed by the 64-byte fingerprint)
+__global__ void __launch_bounds__(256) zc_probe_kernel(const uint8_t* __restrict__ data, AnchorView av,
+                                                       uint64_t nwt, const uint64_t* __restrict__ tkeys,
+                                                       const uint32_t* __restrict__ tvals, uint32_t tbits,
+                                                       const uint32_t* __restrict__ anc_off,
+                                                       const uint64_t* __restrict__ cfp,
+                                                       const uint64_t* __restrict__ vis,
+                                                       const uint8_t* __restrict__ dead, uint64_t r, uint64_t n,
+                                                       uint32_t W, Cand* __restrict__ cand, uint64_t cand_cap,
+                                                       unsigned long long* __restrict__ counters) {
+  const uint64_t wt = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (wt >= nwt) return;
+  const TileAnchors ta = tile_anchors(av, wt);
   const uint32_t mask = (1u << tbits) - 1;
-  for (uint32_t e = 0; e < sa.cnt; ++e) {
-    const uint64_t pos = sx * ZC_LSPAN + sa.rel(e);
+  for (uint32_t e = lane; e < ta.cnt; e += 64) {
+    const uint64_t pos = (wt << ZC_WT_SHIFT) + ta.rel[e];
     if (pos < r + ZC_ANCHOR_MIN_OFF) continue;
-    const uint64_t k = sa.g(e);
-    uint32_t h = table_slot(sa.g(e), tbits);
+    const uint32_t gk = ta.g[e];
+    const uint64_t k = gk;
+    uint32_t h = table_slot(gk, tbits);
     bool have_fp = false;
     uint64_t fp = 0;
     for (;;) {
-      uint64_t tk = tkeys[h];
+      const uint64_t tk = tkeys[h];
       if (tk == kEmpty) break;
       if (tk == k) {
-        uint32_t ref = tvals[h];
-        uint64_t o = anc_off[ref];
+        const uint32_t ref = tvals[h];
+        const uint64_t o = anc_off[ref];
         if (pos >= r + o) {
-          uint64_t ws = pos - o, p = ws + W - 1;
+          const uint64_t ws = pos - o, p = ws + W - 1;
           if (p < n && p >= vis[ref] && !dead[ref]) {
             if (!have_fp) {
               fp = anchor_fp(data, pos);
               have_fp = true;
             }
             if (fp == cfp[ref]) {
-              unsigned long long slot = atomicAdd(&counters[CNT_CAND], 1ull);
+              const unsigned long long slot = atomicAdd(&counters[CNT_CAND], 1ull);
               if (slot < cand_cap) {
                 cand[slot].p = p;
                 cand[slot].ref = ref;
@@ -783,15 +856,8 @@ __global__ void zc_probe_kernel(const uint8_t* __restrict__ data, AnchorView av,
 
 // ---------------------------------------------------------------------------
 // zc_verify: one wave per pair, byte-exact equality of two len-byte ranges
-__global__ void __launch_bounds__(256) zc_verify_kernel(const uint8_t* __restrict__ data,
-                                                        const uint64_t* __restrict__ win_start,
-                                                        const uint64_t* __restrict__ ref_start,
-                                                        uint32_t len, uint32_t npairs,
-                                                        uint8_t* __restrict__ ok) {
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  if (wave >= npairs) return;
-  const uint64_t a = win_start[wave], b = ref_start[wave];
+__device__ __forceinline__ bool wave_ranges_equal(const uint8_t* __restrict__ data, uint64_t a, uint64_t b,
+                                                  uint32_t len, uint32_t lane) {
   bool diff = false;
   uint32_t i = lane * 16;
   for (; i + 16 <= len; i += 64 * 16) {
@@ -801,11 +867,76 @@ __global__ void __launch_bounds__(256) zc_verify_kernel(const uint8_t* __restric
     diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
   }
   // ragged tail (len not a multiple of 16)
-  uint32_t tail0 = len & ~15u;
+  const uint32_t tail0 = len & ~15u;
   for (uint32_t j = tail0 + lane; j < len; j += 64) diff |= data[a + j] != data[b + j];
-  bool any = __any(diff);
-  if (lane == 0) ok[wave] = any ? 0 : 1;
+  return !__any(diff);
 }
+
+__global__ void __launch_bounds__(256) zc_verify_kernel(const uint8_t* __restrict__ data,
+                                                        const uint64_t* __restrict__ win_start,
+                                                        const uint64_t* __restrict__ ref_start,
+                                                        uint32_t len, uint32_t npairs,
+                                                        uint8_t* __restrict__ ok) {
+  const uint32_t wave = (uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (wave >= npairs) return;
+  const bool eq = wave_ranges_equal(data, win_start[wave], ref_start[wave], len, lane);
+  if (lane == 0) ok[wave] = eq ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// content classes: refs whose 64-bit keys are equal and whose bytes are equal
+// form one class, led by its lowest ref index; only leaders enter the anchor
+// table and the exact screen, so repeated content costs one candidate per
+// window instead of one per identical chunk
+__device__ __forceinline__ uint32_t key_slot(uint64_t k, uint32_t bits) {
+  return (uint32_t)((k * kGolden) >> (64 - bits));
+}
+
+__global__ void zc_class_insert_kernel(const uint64_t* __restrict__ key, uint32_t nref, uint64_t* ckeys,
+                                       uint32_t* cvals, uint32_t cbits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nref) return;
+  const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
+  const uint32_t mask = (1u << cbits) - 1;
+  for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&ckeys[h], (unsigned long long)kEmpty,
+                                              (unsigned long long)k);
+    if (prev == kEmpty || prev == k) {
+      atomicMin(&cvals[h], i);
+      return;
+    }
+  }
+}
+
+// one wave per ref: its class = the lowest ref with the same key if the bytes
+// are equal (else itself); counts the refs that are not leaders
+__global__ void __launch_bounds__(256) zc_class_resolve_kernel(const uint8_t* __restrict__ data,
+                                                               const uint64_t* __restrict__ key,
+                                                               const uint64_t* __restrict__ start, uint32_t nref,
+                                                               uint32_t W, const uint64_t* __restrict__ ckeys,
+                                                               const uint32_t* __restrict__ cvals, uint32_t cbits,
+                                                               uint32_t* __restrict__ cls,
+                                                               unsigned long long* __restrict__ counters) {
+  const uint32_t i = (uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (i >= nref) return;
+  const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
+  const uint32_t mask = (1u << cbits) - 1;
+  uint32_t h = key_slot(k, cbits);
+  while (ckeys[h] != k) h = (h + 1) & mask;
+  const uint32_t lead = cvals[h];
+  if (lead == i) {
+    if (lane == 0) cls[i] = i;
+    return;
+  }
+  const bool same = wave_ranges_equal(data, start[i], start[lead], W, lane);
+  if (lane == 0) {
+    cls[i] = same ? lead : i;
+    if (same) atomicAdd(&counters[CNT_CLASS], 1ull);
+  }
+}
+
 
 // ---------------------------------------------------------------------------
 // zc_range_digest: RollingHash::digest of [a, b) = 257^(b-a) + acc
@@ -1114,27 +1245,26 @@ static int cu_count() {
   return cus;
 }
 
-hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, uint16_t* arel,
-                       uint32_t* ag, uint32_t* acnt, uint32_t* ovf_list, uint32_t ovf_cap,
+hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s) {
   const uint64_t nfull = n / ZC_STILE;
   if (nfull) {
     const unsigned grid = (unsigned)std::min<uint64_t>(nfull, (uint64_t)cu_count());
-    hipLaunchKernelGGL(zc_scan_kernel<0>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, nfull, anchor_lo, blk,
-                       arel, ag, acnt, ovf_list, ovf_cap, counters);
+    hipLaunchKernelGGL(zc_scan_kernel<0>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, nfull, anchor_lo, blk, po,
+                       counters);
   }
   if (n % ZC_STILE)
-    hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(1), dim3(ZC_SCAN_TPB), 0, s, data, n, nfull, anchor_lo, blk,
-                       arel, ag, acnt, ovf_list, ovf_cap, counters);
+    hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(ZC_SCAN_TPB / 64), dim3(ZC_TPB), 0, s, data, n, nfull, anchor_lo,
+                       blk, po, counters);
   return hipGetLastError();
 }
 
-hipError_t launch_anchor_dense(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* spans,
-                               uint32_t nspans, const uint64_t* offs, uint64_t* ovf_off, uint16_t* orel,
-                               uint32_t* og, hipStream_t s) {
-  if (!nspans) return hipSuccess;
-  hipLaunchKernelGGL(zc_anchor_dense_kernel, dim3(blocks_for(nspans, 64)), dim3(64), 0, s, data, n, anchor_lo,
-                     spans, nspans, offs, ovf_off, orel, og);
+hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* tiles,
+                                const uint32_t* sbase, uint32_t ntiles, int pass, uint32_t* base, uint32_t* cnt,
+                                uint32_t* srel, uint32_t* sg, hipStream_t s) {
+  if (!ntiles) return hipSuccess;
+  hipLaunchKernelGGL(zc_anchor_rescan_kernel, dim3(ntiles), dim3(ZC_TPB), 0, s, data, n, anchor_lo, tiles, sbase,
+                     pass, base, cnt, srel, sg);
   return hipGetLastError();
 }
 
@@ -1148,10 +1278,10 @@ hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* bl
   return hipGetLastError();
 }
 
-hipError_t launch_anchorless(const uint32_t* anc_off, uint32_t nref, uint32_t* list, uint32_t cap,
-                             unsigned long long* counters, hipStream_t s) {
+hipError_t launch_anchorless(const uint32_t* anc_off, const uint32_t* cls, uint32_t nref, uint32_t* list,
+                             uint32_t cap, unsigned long long* counters, hipStream_t s) {
   if (!nref) return hipSuccess;
-  hipLaunchKernelGGL(zc_anchorless_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, anc_off, nref, list,
+  hipLaunchKernelGGL(zc_anchorless_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, anc_off, cls, nref, list,
                      cap, counters);
   return hipGetLastError();
 }
@@ -1162,20 +1292,35 @@ hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s) {
 }
 
 hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits, const uint32_t* cg,
-                               const uint32_t* anc_off, uint32_t nrefs, hipStream_t s) {
+                               const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs, hipStream_t s) {
   if (!nrefs) return hipSuccess;
   hipLaunchKernelGGL(zc_table_insert_kernel, dim3(blocks_for(nrefs, 256)), dim3(256), 0, s, tkeys,
-                     tvals, tbits, cg, anc_off, nrefs);
+                     tvals, tbits, cg, anc_off, cls, nrefs);
   return hipGetLastError();
 }
 
-hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nspans, const uint64_t* tkeys,
+hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64_t* start, uint32_t nref, uint32_t W,
+                          uint64_t* ckeys, uint32_t* cvals, uint32_t cbits, uint32_t* cls,
+                          unsigned long long* counters, hipStream_t s) {
+  if (!nref) return hipSuccess;
+  const uint32_t csize = 1u << cbits;
+  hipLaunchKernelGGL(zc_table_clear_kernel, dim3(blocks_for(csize, 256)), dim3(256), 0, s, ckeys, csize);
+  hipError_t e = hipMemsetAsync(cvals, 0xFF, csize * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(zc_class_insert_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, key, nref, ckeys, cvals,
+                     cbits);
+  hipLaunchKernelGGL(zc_class_resolve_kernel, dim3(blocks_for((uint64_t)nref * 64, 256)), dim3(256), 0, s, data,
+                     key, start, nref, W, ckeys, cvals, cbits, cls, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tkeys,
                         const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp,
-                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t n, uint32_t W,
-                        Cand* cand, uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
-  if (!nspans) return hipSuccess;
-  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(nspans, 256)), dim3(256), 0, s, data, av, nspans,
-                     tkeys, tvals, tbits, anc_off, cfp, vis, dead, r, n, W, cand, cand_cap, counters);
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t n, uint32_t W, Cand* cand,
+                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
+  if (!nwt) return hipSuccess;
+  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(nwt * 64, 256)), dim3(256), 0, s, data, av, nwt, tkeys,
+                     tvals, tbits, anc_off, cfp, vis, dead, r, n, W, cand, cand_cap, counters);
   return hipGetLastError();
 }
 
