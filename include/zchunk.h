@@ -21,6 +21,8 @@
  *                          (one per BackupInstruction, zbackup.proto:149-159)
  *                                                                backup_creator.hh:89 / .cc:275-280
  *   zc_chunk_device        the same stream already resident in HBM (feed + finish in one call)
+ *   zc_chunk_host          the same stream in host memory, copy overlapped with the scan
+ *                          (the read loop of zutils.cc:100-124 + finish in one call)
  *   zc_last_error          the DEF_EX exceptions / CHECK aborts of the reference
  *                          (backup_creator.cc:112,165-166, chunk_index.hh:88-89)
  */
@@ -108,6 +110,12 @@ int zc_finish(zc_ctx* ctx);
  * The context's stream is ordered after work already queued on the legacy
  * default stream (so a buffer just written there is read complete). */
 int zc_chunk_device(zc_ctx* ctx, const void* d_data, uint64_t n);
+
+/* stream in host memory (pinned for full speed): copied to HBM in 64 MiB
+ * segments on a side stream, each segment scanned as soon as it has landed,
+ * then the same pipeline as zc_chunk_device; the end-to-end form of
+ * backup_creator.cc's loop, with the feed's copies overlapped with the work */
+int zc_chunk_host(zc_ctx* ctx, const void* host, uint64_t n);
 
 size_t zc_record_count(const zc_ctx* ctx);
 int zc_get_records(const zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);

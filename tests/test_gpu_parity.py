@@ -150,6 +150,18 @@ def test_dense_anchor_overflow_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
+def test_chunk_host_overlapped_vs_oracle(torch_cuda):
+    # zc_chunk_host: several 64 MiB copy/scan segments plus a partial tile,
+    # from pinned host memory; records equal the oracle's
+    from zbackup_amd import BackupCreator
+    data = oracle.gen("R5:80000000,C1000:50000000,Z:3000000,R6:7777777")
+    want = oracle.chunk(data, W64)
+    host = torch_cuda.from_numpy(data).pin_memory()
+    with BackupCreator(W64) as bc:
+        bc.chunk_host(host.data_ptr(), data.size)
+        assert bc.record_tuples() == want
+
+
 def test_index_persists_across_streams(torch_cuda):
     # ChunkStorage::Writer::add -> ChunkIndex::addChunk: a second stream on the
     # same context matches the first stream's chunks (zutils.cc:137-166 reuses

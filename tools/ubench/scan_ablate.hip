@@ -22,9 +22,10 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&prel, nwt * wcap * 4)); CK(hipMalloc(&pg, nwt * wcap * 4)); CK(hipMalloc(&cnt, 64));
   const PoolOut po{dbase, dcnt, prel, pg, wcap};
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-  struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
+  struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
   std::vector<V> vs = {
     {"full", zc_scan_kernel<0>, {}},
+    {"full_defer", zc_scan_kernel<ABL_DEFER>, {}},
     {"no_record", zc_scan_kernel<ABL_NO_RECORD>, {}},
     {"no_digest", zc_scan_kernel<ABL_NO_DIGEST>, {}},
     {"no_digest_no_record", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_RECORD>, {}},
@@ -41,7 +42,7 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
       CK(hipMemset(cnt, 0, 64));
       CK(hipEventRecord(a));
-      hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, ntiles, anchor_lo_for(65536), blk, po, cnt);
+      hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, (uint64_t)0, ntiles, anchor_lo_for(65536), blk, po, cnt);
       CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
       float ms; CK(hipEventElapsedTime(&ms, a, b));
       if (round) v.t.push_back(ms);

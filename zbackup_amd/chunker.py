@@ -105,6 +105,12 @@ class BackupCreator:
         _check(self._L, self._ctx, self._L.zc_chunk_device(self._ctx, ctypes.c_void_p(ptr), n),
                "zc_chunk_device")
 
+    def chunk_host(self, ptr, n):
+        """Process `n` bytes in host memory at address `ptr` (pinned for full
+        speed): HBM copies in 64 MiB segments overlapped with the scan, then
+        the same pipeline as chunk_device (zutils.cc:100-124 read loop + finish)."""
+        _check(self._L, self._ctx, self._L.zc_chunk_host(self._ctx, ctypes.c_void_p(ptr), n), "zc_chunk_host")
+
     # -- results -------------------------------------------------------------
     def records(self):
         n = self._L.zc_record_count(self._ctx)

@@ -14,17 +14,35 @@ namespace zc {
 constexpr int ZC_SPAN = 1024;                                // digest granularity
 constexpr int ZC_TPB = 256;                                  // 4 waves
 // zc_scan: 512-lane persistent workgroups, lane span 4 KiB (2 MiB tiles),
-// per-wave LDS rings of ZC_RING slots of 128-byte rounds
-constexpr int ZC_SCAN_TPB = 512;
-constexpr int ZC_LSPAN = 4096;
+// per-wave LDS rings of ZC_RING slots of 128-byte rounds.  (The *_CFG macros
+// exist for the geometry sweeps of tools/ubench/scan_ablate.hip.)
+#ifndef ZC_SCAN_TPB_CFG
+#define ZC_SCAN_TPB_CFG 512
+#endif
+#ifndef ZC_LSPAN_CFG
+#define ZC_LSPAN_CFG 4096
+#endif
+#ifndef ZC_ROUND_CFG
+#define ZC_ROUND_CFG 128
+#endif
+#ifndef ZC_WLIST_CFG
+#define ZC_WLIST_CFG 144
+#endif
+constexpr int ZC_SCAN_TPB = ZC_SCAN_TPB_CFG;
+constexpr int ZC_LSPAN = ZC_LSPAN_CFG;
 constexpr uint64_t ZC_STILE = (uint64_t)ZC_LSPAN * ZC_SCAN_TPB;
-constexpr int ZC_ROUND = 128;
+constexpr int ZC_ROUND = ZC_ROUND_CFG;
 constexpr int ZC_RING = 2;
-constexpr int ZC_WLIST = 144;                                // per-wave LDS list of pieces with anchors
+constexpr int ZC_WLIST = ZC_WLIST_CFG;                       // per-wave LDS list of pieces with anchors
+static_assert(ZC_LSPAN % ZC_SPAN == 0 && ZC_LSPAN / ZC_SPAN % 2 == 0 && ZC_LSPAN <= 4096, "lane span");
+static_assert(ZC_ROUND >= 64 && ZC_ROUND <= 256 && ZC_SPAN % ZC_ROUND == 0, "round");
 // wave-tile: the 64 lane spans (256 KiB) one scan wave covers per tile;
 // wave-tile t holds stream positions [t << ZC_WT_SHIFT, (t + 1) << ZC_WT_SHIFT)
-constexpr int ZC_WT_SHIFT = 18;
+constexpr int ilog2_c(uint64_t v) { return v <= 1 ? 0 : 1 + ilog2_c(v >> 1); }
+constexpr int ZC_WT_SHIFT = ilog2_c(64ull * ZC_LSPAN);
 static_assert((64ull * ZC_LSPAN) == (1ull << ZC_WT_SHIFT), "wave-tile = 64 lane spans");
+// threads of the blocks that process one wave-tile bytewise, a 1 KiB sub-span each
+constexpr int ZC_WT_BLOCK = (1 << ZC_WT_SHIFT) / ZC_SPAN;
 // zc_fscan: lane span 1 KiB, 256 KiB per workgroup
 constexpr uint64_t ZC_TILE = (uint64_t)ZC_SPAN * ZC_TPB;
 constexpr int ZC_RUN_SLOTS = 4;                              // LDS screen-run slots per lane
@@ -97,6 +115,12 @@ enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4,
 // --- launchers (return hipError_t of the launch) ---------------------------
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s);
+// the same in pieces: full 2 MiB tiles [tile0, tile0 + ntiles), then the
+// partial last tile (if any); the pieces may run as the stream arrives
+hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s);
+hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
+                            unsigned long long* counters, hipStream_t s);
 
 // exact rescan of the wave-tiles the scan marked overflowed (directory count
 // 0xFFFFFFFF): pass 0 sets cnt[tiles[i]] to the exact count; pass 1 writes the

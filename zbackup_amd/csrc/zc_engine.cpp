@@ -121,6 +121,7 @@ struct StaticEntry {
 constexpr uint64_t kInf = ~0ull;
 constexpr size_t kFeedChunk = 8u << 20;
 constexpr size_t kFBatchMax = 1u << 20;
+constexpr uint64_t kHostSegment = 64ull << 20;  // zc_chunk_host copy/scan pipeline granularity
 
 }  // namespace
 
@@ -129,6 +130,7 @@ struct zc_ctx {
   uint32_t W = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_in = nullptr;
   std::string err;
 
@@ -197,14 +199,37 @@ class Resolver {
   Resolver(zc_ctx& c, const uint8_t* d, uint64_t n)
       : c_(c), d_(d), n_(n), W_(c.W), indexable_(c.W >= 128) {}
 
+  // whole pipeline over a stream already in HBM
   void run() {
-    auto t0 = std::chrono::steady_clock::now();
+    begin();
+    resolve();
+  }
+
+  // Pipeline over a stream arriving in HBM piece by piece: begin(), then
+  // scan_upto(m) as the first m bytes land (in order, on the context's
+  // stream), then resolve() once all n bytes are queued.
+  void begin() {
+    t_begin_ = Clock::now();
     c_.recs.clear();
     c_.recs.reserve(std::min<uint64_t>(n_ / W_ + 16, 1u << 24));
     c_.stats = zc_stats{};
     c_.stats.bytes = n_;
     if (n_ == 0) return;
-    scan();
+    scan_setup();
+  }
+  void scan_upto(uint64_t m) {
+    const uint64_t t1 = std::min(m, n_) / ZC_STILE;
+    if (t1 > tiles_done_) {
+      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, c_.blk.p, pool_out(), c_.counters.p,
+                            c_.stream));
+      tiles_done_ = t1;
+    }
+  }
+  void resolve() {
+    if (n_ == 0) return;
+    scan_upto(n_);
+    HCK(launch_scan_tail(d_, n_, anchor_lo_, c_.blk.p, pool_out(), c_.counters.p, c_.stream));
+    scan_finish();
     auto t1 = std::chrono::steady_clock::now();
     // static entries keyed by rolling hash
     for (size_t i = 0; i < c_.statics.size(); ++i) smap_[c_.statics[i].key].push_back((uint32_t)i);
@@ -215,7 +240,7 @@ class Resolver {
     finalize();
     auto t2 = std::chrono::steady_clock::now();
     c_.stats.resolve_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    c_.stats.total_ms = std::chrono::duration<double, std::milli>(t2 - t0).count();
+    c_.stats.total_ms = std::chrono::duration<double, std::milli>(t2 - t_begin_).count();
   }
 
  private:
@@ -227,7 +252,12 @@ class Resolver {
   uint64_t npool_ = 0;
   uint64_t nwt_ = 0;  // wave-tiles of the stream
   const int32_t anchor_lo_ = anchor_lo_for(W_);
+  const uint32_t wcap_ = wave_tile_cap(W_);
   AnchorView av_{};
+  Clock::time_point t_begin_;
+  uint64_t tiles_done_ = 0;  // full scan tiles launched
+
+  PoolOut pool_out() { return PoolOut{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, wcap_}; }
 
   // resolver state
   uint64_t r_ = 0, s_ = 0, r_e_ = 0;
@@ -311,21 +341,21 @@ class Resolver {
   std::vector<Piece> need_digest_;
 
   // ---------------------------------------------------------------- scan
-  void scan() {
+  void scan_setup() {
     nwt_ = wave_tiles(n_);
-    const uint32_t wcap = wave_tile_cap(W_);
-    if (nwt_ * wcap >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "stream too large for the anchor pool"};
+    if (nwt_ * wcap_ >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "stream too large for the anchor pool"};
     c_.blk.ensure((n_ + ZC_SPAN - 1) / ZC_SPAN);
     c_.dbase.ensure(nwt_);
     c_.dcnt.ensure(nwt_);
-    c_.prel.ensure(nwt_ * wcap);
-    c_.pg.ensure(nwt_ * wcap);
+    c_.prel.ensure(nwt_ * wcap_);
+    c_.pg.ensure(nwt_ * wcap_);
     c_.counters.ensure(CNT_LAST);
     c_.h_cnt.ensure(CNT_LAST);
     HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
     if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
-    HCK(launch_scan(d_, n_, anchor_lo_, c_.blk.p, PoolOut{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, wcap},
-                    c_.counters.p, c_.stream));
+  }
+
+  void scan_finish() {
     if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
     d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
     sync(c_);
@@ -509,9 +539,31 @@ class Resolver {
     acands_.reserve(nc);
     for (uint64_t i = 0; i < nc; ++i)
       if (ok[i]) acands_.push_back({hc[i].p, hc[i].ref});
-    std::sort(acands_.begin(), acands_.end(), [](const ACand& a, const ACand& b) {
-      return a.p != b.p ? a.p < b.p : a.ref < b.ref;
-    });
+    sort_by_position(acands_);
+  }
+
+  // LSD radix sort by window end (11-bit digits, stable).  Candidates with the
+  // same end are windows equal to refs of equal content, so their relative
+  // order does not change the walk.
+  void sort_by_position(std::vector<ACand>& v) {
+    const size_t m = v.size();
+    if (m < 2) return;
+    std::vector<ACand> tmp(m);
+    uint32_t bits = 1;
+    while (bits < 64 && (n_ >> bits)) ++bits;
+    std::vector<uint32_t> cnt(2048);
+    for (uint32_t shift = 0; shift < bits; shift += 11) {
+      std::fill(cnt.begin(), cnt.end(), 0u);
+      for (const ACand& a : v) ++cnt[(a.p >> shift) & 2047];
+      uint32_t sum = 0;
+      for (uint32_t& c : cnt) {
+        const uint32_t t = c;
+        c = sum;
+        sum += t;
+      }
+      for (const ACand& a : v) tmp[cnt[(a.p >> shift) & 2047]++] = a;
+      v.swap(tmp);
+    }
   }
 
   std::vector<uint8_t> verify_pairs(const std::vector<uint64_t>& wa, const std::vector<uint64_t>& ra,
@@ -984,6 +1036,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
   int rc = guarded(c, [&] {
     DeviceGuard g(device);
     HCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HCK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     HCK(hipEventCreate(&c->ev0));
     HCK(hipEventCreate(&c->ev1));
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
@@ -1008,6 +1061,8 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -1074,6 +1129,35 @@ int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
     Resolver res(*c, (const uint8_t*)d_data, n);
     res.run();
     c->d_last = (const uint8_t*)d_data;
+    c->n_last = n;
+    c->finished = true;
+  });
+}
+
+int zc_chunk_host(zc_ctx* c, const void* host, uint64_t n) {
+  if (!c || (n && !host)) return ZC_ERR_ARG;
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    if (c->d_stream.cap < n) {
+      c->d_stream.release();
+      c->d_stream.ensure((n + 4095) & ~uint64_t(4095));
+    }
+    c->n_stream = n;
+    uint8_t* d = c->d_stream.p;
+    const uint8_t* h = (const uint8_t*)host;
+    // segments land on the copy stream; the scan of each follows on the
+    // context's stream as soon as its copy has completed
+    Resolver res(*c, d, n);
+    res.begin();
+    for (uint64_t off = 0; off < n; off += kHostSegment) {
+      const uint64_t len = std::min<uint64_t>(kHostSegment, n - off);
+      HCK(hipMemcpyAsync(d + off, h + off, len, hipMemcpyHostToDevice, c->copy_stream));
+      HCK(hipEventRecord(c->ev_in, c->copy_stream));
+      HCK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
+      res.scan_upto(off + len);
+    }
+    res.resolve();
+    c->d_last = d;
     c->n_last = n;
     c->finished = true;
   });

@@ -51,9 +51,9 @@ __host__ __device__ inline uint64_t pow257_dev(uint64_t e) {
 // 257^ZC_SPAN mod 2^64, the multiplier that appends one whole span digest
 __device__ __forceinline__ uint64_t span_mul() { return pow257_dev(ZC_SPAN); }
 
-// Exclusive prefix sum over the 256 threads of a block.
+// Exclusive prefix sum over the threads of a block (at most 1024).
 __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   uint32_t x = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -63,8 +63,7 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total
   if (lane == 63) s_tmp[wid] = x;
   __syncthreads();
   uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < ZC_TPB / 64; ++w) {
+  for (int w = 0; w < nw; ++w) {
     uint32_t t = s_tmp[w];
     pre += (w < wid) ? t : 0u;
     tot += t;
@@ -178,9 +177,11 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 // 8 = skip the per-byte work entirely (staging + reads only),
 // 16 = gear + max computed but folded into the state without a ballot/branch,
 // 32 = anchor threshold raised so the recording block is (almost) never taken,
-// 64 = no tile-end work (span digests, anchor slots)
+// 64 = no tile-end work (span digests, anchor slots),
+// 128 = anchor test per piece without a branch, recording deferred to the
+// end of the round
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32, ABL_NO_TILE_END = 64 };
+       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_DEFER = 128 };
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
   uint32_t* e;      // {lane << 16 | rel of the piece, gear before the piece}
@@ -213,7 +214,7 @@ __device__ __forceinline__ void add64_pair(uint32_t& hlo, uint32_t& hhi, uint32_
 // list, and the tile end re-derives the exact anchors from those 16 bytes.
 template <int ABL>
 __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane, int32_t lo_thr,
-                                           ScanLane& s, WaveList& wl) {
+                                           ScanLane& s, WaveList& wl, uint64_t* defer = nullptr) {
   const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
   if (ABL & ABL_NO_BYTES) {
     s.hlo ^= xs[0] ^ xs[1] ^ xs[2] ^ xs[3];
@@ -251,6 +252,10 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane,
   }
   if (ABL & ABL_NEVER) lo_thr = 0x7FFFFFFF;
   const uint64_t any = __ballot(m >= lo_thr);
+  if (ABL & ABL_DEFER) {
+    *defer = any;
+    return;
+  }
   if (__builtin_expect(any != 0, 0)) {
     if (ABL & ABL_NO_RECORD) {
       wl.n += __popcll(any);
@@ -336,7 +341,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
 __device__ uint32_t wave_tile_block(const uint8_t* __restrict__ data, uint64_t n, uint64_t wt, int32_t lo_thr,
                                     uint64_t* __restrict__ blk, uint32_t* __restrict__ rel,
                                     uint32_t* __restrict__ g, uint32_t base, uint32_t cap, uint32_t* s_tmp) {
-  static_assert((ZC_TPB * ZC_SPAN) == (1 << ZC_WT_SHIFT), "a block covers a wave-tile");
+  // blockDim.x == ZC_WT_BLOCK: the block covers the wave-tile
   const uint64_t t0 = wt << ZC_WT_SHIFT, q0 = t0 + (uint64_t)threadIdx.x * ZC_SPAN;
   uint32_t cnt = 0;
   if (q0 < n) {
@@ -370,22 +375,28 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int kRounds = ZC_LSPAN / ZC_ROUND;  // rounds per tile (plus one warm-up round)
 constexpr int kDmaRound = 64 * ZC_ROUND / 1024;  // DMA instructions per wave-round
 constexpr int kDmaWarm = 2;                      // ... per warm-up round (64 x 32 B)
+constexpr int kDigests = ZC_LSPAN / ZC_SPAN;     // span digests per lane span
 
-// DMA of round r of `tile` into ring slot `slot`: ZC_ROUND = 128 bytes of each
-// of the wave's 64 rows; one instruction fills 8 rows (1 KiB); swizzle
-// (row >> 1) & 7.  The per-lane part of the source address is loop-invariant
-// (off_even / off_odd); the rest is wave-uniform.
+// LDS image of a wave-round: row i (lane i's ZC_ROUND bytes) is stored
+// linearly, with its 16-byte piece p at position p ^ swz(i); the swizzle makes
+// the per-lane ds_read_b128 of a row bank-conflict free (rows within one
+// 256-byte bank stripe get distinct piece positions).
+constexpr int kPieces = ZC_ROUND / 16;
+__host__ __device__ constexpr uint32_t row_swizzle(uint32_t row) { return (row / (256 / ZC_ROUND)) % kPieces; }
+
+// DMA of round r of `tile` into ring slot `slot`: ZC_ROUND bytes of each of
+// the wave's 64 rows; one instruction fills 1024 / ZC_ROUND rows (1 KiB).
+// The per-lane part of the source address (lane_off[j]) is loop-invariant;
+// the rest is wave-uniform.
 __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
-                                            uint32_t off_even, uint32_t off_odd, uint64_t tile, int r,
+                                            const uint32_t (&lane_off)[kDmaRound], uint64_t tile, int r,
                                             uint32_t slot) {
   uint8_t* dst = ring + slot * (64 * ZC_ROUND);
-  const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN;
+  const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)r * ZC_ROUND;
 #pragma unroll
-  for (int j = 0; j < kDmaRound; ++j) {
-    const uint8_t* base = data + tile0 + (uint64_t)j * (1024 / ZC_ROUND) * ZC_LSPAN + (uint64_t)r * ZC_ROUND;
-    const uint32_t lane_off = (j & 1) ? off_odd : off_even;
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + lane_off), (lds_void_t*)(dst + j * 1024), 16, 0, 0);
-  }
+  for (int j = 0; j < kDmaRound; ++j)
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + tile0 + lane_off[j]), (lds_void_t*)(dst + j * 1024), 16,
+                                     0, 0);
 }
 
 // DMA of the warm-up round of `tile`: the 32 bytes before each of the wave's
@@ -438,13 +449,14 @@ constexpr uint32_t ZC_WT_OVERFLOW = 0xFFFFFFFFu;
 // the list; a wave-tile whose list or pool share overflowed is marked for the
 // exact rescan (zc_anchor_rescan) and stores nothing.
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
-                                                  const uint64_t (&bk)[4], const WaveList& wl,
+                                                  const uint64_t (&bk)[kDigests], const WaveList& wl,
                                                   uint64_t* __restrict__ blk, PoolOut po,
                                                   unsigned long long* __restrict__ counters) {
-  static_assert(ZC_LSPAN / ZC_SPAN == 4, "four span digests per lane span");
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
-  bo[0] = make_uint4((uint32_t)bk[0], (uint32_t)(bk[0] >> 32), (uint32_t)bk[1], (uint32_t)(bk[1] >> 32));
-  bo[1] = make_uint4((uint32_t)bk[2], (uint32_t)(bk[2] >> 32), (uint32_t)bk[3], (uint32_t)(bk[3] >> 32));
+#pragma unroll
+  for (int t = 0; t < kDigests / 2; ++t)
+    bo[t] = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
+                       (uint32_t)(bk[2 * t + 1] >> 32));
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)wt * po.wcap;
   if (wl.n > ZC_WLIST) {
@@ -535,7 +547,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   }
   const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
   const bool slow = cnt > (uint32_t)kTileSlots;
-  uint32_t nstores = 2;  // the digests
+  uint32_t nstores = kDigests / 2;  // the digests
   // 3) the common case's pool stores: one instruction pair per slot level
   //    some lane reaches
 #pragma unroll
@@ -573,38 +585,41 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
 // wave computes.
 template <int ABL>
 __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t nfull, int32_t lo_thr,
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
   __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
   __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
   constexpr uint32_t kRpt = kRounds + 1;  // rounds per tile, warm-up included
-  constexpr int kPieces = ZC_ROUND / 16;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t grid = gridDim.x;
   uint8_t* myring = ring[wave];
   WaveList wl{wlist[wave], wdata[wave], 0};
-  const uint32_t ntk = nfull > blockIdx.x ? (uint32_t)((nfull - 1 - blockIdx.x) / grid + 1) : 0;
+  const uint32_t ntk = ntiles > blockIdx.x ? (uint32_t)((ntiles - 1 - blockIdx.x) / grid + 1) : 0;
   const uint32_t nR = ntk * kRpt;
-  // this lane's share of DMA instruction j: row j * 8 + lane / 8 of the wave,
-  // piece (lane % 8) ^ ((row >> 1) & 7); the swizzle term is (lane / 16) ^ 4 * (j & 1)
-  const uint32_t drow = lane / (ZC_ROUND / 16);
-  const uint32_t dpiece = (lane % (ZC_ROUND / 16)) ^ ((drow >> 1) & 7);
-  const uint32_t off_even = drow * ZC_LSPAN + dpiece * 16;
-  const uint32_t off_odd = drow * ZC_LSPAN + (dpiece ^ 4) * 16;
-  const uint32_t sw = (lane >> 1) & 7;  // read-side swizzle of this lane's row
+  // this lane's share of DMA instruction j: row j * (1024 / ZC_ROUND) + lane /
+  // kPieces of the wave, the source piece that lands at position lane % kPieces
+  uint32_t lane_off[kDmaRound];
+#pragma unroll
+  for (int j = 0; j < kDmaRound; ++j) {
+    const uint32_t row = j * (1024 / ZC_ROUND) + lane / kPieces;
+    lane_off[j] = row * ZC_LSPAN + ((lane % kPieces) ^ row_swizzle(row)) * 16;
+  }
+  const uint32_t sw = row_swizzle(lane);  // read-side swizzle of this lane's row
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kRpt, r1 = Rx - k * kRpt;
-    const uint64_t tile = blockIdx.x + (uint64_t)k * grid;
+    const uint64_t tile = tile0 + blockIdx.x + (uint64_t)k * grid;
     if (r1 == 0)
       stage_warmup(data, myring, wave, lane, tile, Rx & 1);
     else
-      stage_round(data, myring, wave, off_even, off_odd, tile, (int)r1 - 1, Rx & 1);
+      stage_round(data, myring, wave, lane_off, tile, (int)r1 - 1, Rx & 1);
   };
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
   ScanLane s{0, 0, 0};
-  uint64_t bk[4] = {0, 0, 0, 0};
+  uint64_t bk[kDigests];
+#pragma unroll
+  for (int t = 0; t < kDigests; ++t) bk[t] = 0;
   uint64_t span0 = 0;
   uint32_t tail_stores = 0;  // global stores the last tile end left in flight
 
@@ -623,7 +638,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       const uint4 w0 = *(const uint4*)(row + lane * 32), w1 = *(const uint4*)(row + lane * 32 + 16);
       wait_lgkmcnt<0>();  // the slot is free
       if (R + 2 < nR) issue(R + 2);
-      span0 = (blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
+      span0 = (tile0 + blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
       s = ScanLane{0, 0, 0};
       wl.n = 0;
       if (span0 >= 64) {
@@ -640,13 +655,36 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     for (int p = 0; p < kPieces; ++p) v[p] = *(const uint4*)(row + lane * ZC_ROUND + ((p ^ sw) << 4));
     wait_lgkmcnt<0>();  // the slot is free
     if (R + 2 < nR) issue(R + 2);
+    if (ABL & ABL_DEFER) {
+      // the round's pieces hashed without branches; pieces with anchors are
+      // listed afterwards (their bytes and entry gear are still in registers)
+      uint64_t hm[kPieces];
+      uint32_t g0[kPieces];
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lane, lo_thr, s, wl);
+      for (int p = 0; p < kPieces; ++p) {
+        g0[p] = s.glo;
+        scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lane, lo_thr, s, wl, &hm[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p)
+        if (hm[p]) {
+          const uint32_t idx = wl.n + lane_prefix(hm[p]);
+          if (((hm[p] >> lane) & 1) && idx < ZC_WLIST) {
+            wl.e[2 * idx] = (lane << 16) | ((uint32_t)r * ZC_ROUND + p * 16);
+            wl.e[2 * idx + 1] = g0[p];
+            wl.x[idx] = v[p];
+          }
+          wl.n += __popcll(hm[p]);
+        }
+    } else {
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lane, lo_thr, s, wl);
+    }
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const int q = r / (ZC_SPAN / ZC_ROUND);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < kDigests; ++t)
         if (q == t) bk[t] = h;
       s.hlo = s.hhi = 0;
     }
@@ -657,11 +695,11 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
 
 // the stream's last, partial tile: one 256-thread block per wave-tile, a
 // 1 KiB sub-span per thread (block digests and anchors)
-__global__ void __launch_bounds__(ZC_TPB) zc_scan_tail_kernel(const uint8_t* __restrict__ data, uint64_t n,
+__global__ void __launch_bounds__(ZC_WT_BLOCK) zc_scan_tail_kernel(const uint8_t* __restrict__ data, uint64_t n,
                                                              uint64_t tile, int32_t lo_thr,
                                                              uint64_t* __restrict__ blk, PoolOut po,
                                                              unsigned long long* __restrict__ counters) {
-  __shared__ uint32_t s_tmp[ZC_TPB / 64];
+  __shared__ uint32_t s_tmp[ZC_WT_BLOCK / 64];
   const uint64_t wt = tile * (ZC_SCAN_TPB / 64) + blockIdx.x;
   const uint32_t base = (uint32_t)wt * po.wcap;
   const uint32_t tot = wave_tile_block(data, n, wt, lo_thr, blk, po.rel, po.g, base, po.wcap, s_tmp);
@@ -680,13 +718,13 @@ __global__ void __launch_bounds__(ZC_TPB) zc_scan_tail_kernel(const uint8_t* __r
 // Exact rescan of the wave-tiles marked overflowed, one block each: pass 0
 // counts (cnt[wt] = exact count), pass 1 writes the anchors into the side
 // pool at sbase[i] and points the directory there.
-__global__ void __launch_bounds__(ZC_TPB) zc_anchor_rescan_kernel(const uint8_t* __restrict__ data, uint64_t n,
+__global__ void __launch_bounds__(ZC_WT_BLOCK) zc_anchor_rescan_kernel(const uint8_t* __restrict__ data, uint64_t n,
                                                                  int32_t lo_thr, const uint32_t* __restrict__ tiles,
                                                                  const uint32_t* __restrict__ sbase, int pass,
                                                                  uint32_t* __restrict__ dbase,
                                                                  uint32_t* __restrict__ dcnt,
                                                                  uint32_t* __restrict__ srel, uint32_t* __restrict__ sg) {
-  __shared__ uint32_t s_tmp[ZC_TPB / 64];
+  __shared__ uint32_t s_tmp[ZC_WT_BLOCK / 64];
   const uint64_t wt = tiles[blockIdx.x];
   const uint32_t b = pass ? sbase[blockIdx.x] : 0u;
   const uint32_t tot = wave_tile_block(data, n, wt, lo_thr, nullptr, pass ? srel : nullptr, sg, b, ~0u, s_tmp);
@@ -1245,25 +1283,35 @@ static int cu_count() {
   return cus;
 }
 
+hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
+  if (!ntiles) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
+  hipLaunchKernelGGL(zc_scan_kernel<0>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles, anchor_lo, blk,
+                     po, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
+                            unsigned long long* counters, hipStream_t s) {
+  if (n % ZC_STILE)
+    hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(ZC_SCAN_TPB / 64), dim3(ZC_WT_BLOCK), 0, s, data, n, n / ZC_STILE,
+                       anchor_lo, blk, po, counters);
+  return hipGetLastError();
+}
+
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s) {
-  const uint64_t nfull = n / ZC_STILE;
-  if (nfull) {
-    const unsigned grid = (unsigned)std::min<uint64_t>(nfull, (uint64_t)cu_count());
-    hipLaunchKernelGGL(zc_scan_kernel<0>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, nfull, anchor_lo, blk, po,
-                       counters);
-  }
-  if (n % ZC_STILE)
-    hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(ZC_SCAN_TPB / 64), dim3(ZC_TPB), 0, s, data, n, nfull, anchor_lo,
-                       blk, po, counters);
-  return hipGetLastError();
+  hipError_t e = launch_scan_tiles(data, n, 0, n / ZC_STILE, anchor_lo, blk, po, counters, s);
+  if (e != hipSuccess) return e;
+  return launch_scan_tail(data, n, anchor_lo, blk, po, counters, s);
 }
 
 hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_lo, const uint32_t* tiles,
                                 const uint32_t* sbase, uint32_t ntiles, int pass, uint32_t* base, uint32_t* cnt,
                                 uint32_t* srel, uint32_t* sg, hipStream_t s) {
   if (!ntiles) return hipSuccess;
-  hipLaunchKernelGGL(zc_anchor_rescan_kernel, dim3(ntiles), dim3(ZC_TPB), 0, s, data, n, anchor_lo, tiles, sbase,
+  hipLaunchKernelGGL(zc_anchor_rescan_kernel, dim3(ntiles), dim3(ZC_WT_BLOCK), 0, s, data, n, anchor_lo, tiles, sbase,
                      pass, base, cnt, srel, sg);
   return hipGetLastError();
 }
