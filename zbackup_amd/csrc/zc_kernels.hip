@@ -177,14 +177,12 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 // 8 = skip the per-byte work entirely (staging + reads only),
 // 16 = gear + max computed but folded into the state without a ballot/branch,
 // 32 = anchor threshold raised so the recording block is (almost) never taken,
-// 64 = no tile-end work (span digests, anchor slots),
-// 128 = anchor test per piece without a branch, recording deferred to the
-// end of the round
+// 64 = no tile-end work (span digests, anchors to the pool)
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_DEFER = 128 };
+       ABL_NEVER = 32, ABL_NO_TILE_END = 64 };
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
-  uint32_t* e;      // {lane << 16 | rel of the piece, gear before the piece}
+  uint32_t* e;      // {(rel of the piece >> 4) << 8 | the lane's previous entry, gear before the piece}
   uint4* x;         // the piece's 16 bytes
   uint32_t n;       // wave-uniform count (may exceed capacity: then rescan)
 };
@@ -210,11 +208,12 @@ __device__ __forceinline__ void add64_pair(uint32_t& hlo, uint32_t& hhi, uint32_
 // add.  Anchor test: one compare of the piece's max gear and one ballot per
 // piece.  The recording block is wave-uniform (the list count stays scalar)
 // and entered for ~22 % of pieces at the 1/4096 anchor rate: each lane with a
-// hit appends the piece (its bytes and the gear before it) to the wave's LDS
-// list, and the tile end re-derives the exact anchors from those 16 bytes.
+// hit appends the piece (its bytes, the gear before it and a link to the
+// lane's previous entry) to the wave's LDS list, and the tile end re-derives
+// the exact anchors from those 16 bytes.
 template <int ABL>
-__device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane, int32_t lo_thr,
-                                           ScanLane& s, WaveList& wl, uint64_t* defer = nullptr) {
+__device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr, ScanLane& s, WaveList& wl,
+                                           uint32_t& last) {
   const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
   if (ABL & ABL_NO_BYTES) {
     s.hlo ^= xs[0] ^ xs[1] ^ xs[2] ^ xs[3];
@@ -252,10 +251,6 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane,
   }
   if (ABL & ABL_NEVER) lo_thr = 0x7FFFFFFF;
   const uint64_t any = __ballot(m >= lo_thr);
-  if (ABL & ABL_DEFER) {
-    *defer = any;
-    return;
-  }
   if (__builtin_expect(any != 0, 0)) {
     if (ABL & ABL_NO_RECORD) {
       wl.n += __popcll(any);
@@ -263,9 +258,10 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, uint32_t lane,
     }
     const uint32_t idx = wl.n + lane_prefix(any);
     if (m >= lo_thr && idx < ZC_WLIST) {
-      wl.e[2 * idx] = (lane << 16) | rel;
+      wl.e[2 * idx] = ((rel >> 4) << 8) | last;
       wl.e[2 * idx + 1] = g0;
       wl.x[idx] = v;
+      last = idx;
     }
     wl.n += __popcll(any);
   }
@@ -434,23 +430,61 @@ __device__ __forceinline__ void wait_vmcnt_dyn(uint32_t n) {
   }
 }
 
-// anchors of one span kept in registers at the tile end (more: a second pass
-// over the LDS list)
-constexpr int kTileSlots = 6;
 // directory count of a wave-tile left for the exact rescan
 constexpr uint32_t ZC_WT_OVERFLOW = 0xFFFFFFFFu;
+// no list entry (end of a lane's chain)
+constexpr uint32_t kNoEntry = 0xFFu;
+static_assert(ZC_WLIST < kNoEntry, "entry indices fit 8 bits");
 
-// End of a tile: the lane's four span digests; the wave's anchors, from its
-// LDS piece list, to the wave-tile's pool share in position order; the
-// directory entry and the anchor count.  The common case issues a known
-// number of global stores and no waits, and returns that number, so the next
-// round's wait can leave them in flight (an under-count is always safe).
-// Lanes with more than kTileSlots anchors store them in a second pass over
-// the list; a wave-tile whose list or pool share overflowed is marked for the
-// exact rescan (zc_anchor_rescan) and stores nothing.
+// The anchors of list entry i (a 16-byte piece of the lane span at span0):
+// hit mask of its 16 positions (offsets below 63 of the stream excluded) and
+// the gear value of each position, rolled on from the gear before the piece.
+struct PieceHits {
+  uint32_t mask, rel;  // rel: offset of the piece in the lane span
+  uint32_t g0;         // gear before the piece
+  uint32_t xs[4];
+};
+
+__device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, uint64_t span0, int32_t lo_thr) {
+  PieceHits h;
+  const uint32_t e0 = wl.e[2 * i];
+  h.rel = ((e0 >> 8) & 0xFFu) << 4;
+  h.g0 = wl.e[2 * i + 1];
+  const uint4 v = wl.x[i];
+  h.xs[0] = v.x;
+  h.xs[1] = v.y;
+  h.xs[2] = v.z;
+  h.xs[3] = v.w;
+  uint32_t g = h.g0, mask = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t x = h.xs[d];
+    const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
+                            __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
+                            __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mask |= ((int32_t)((g << (k + 1)) + dd[k]) >= lo_thr) ? 1u << (4 * d + k) : 0u;
+    g = (g << 4) + dd[3];
+  }
+  if (span0 + h.rel < ZC_ANCHOR_MIN_OFF)  // the stream's first 63 positions are no anchors
+    mask &= ~0u << min(ZC_ANCHOR_MIN_OFF - (uint32_t)(span0 + h.rel), 16u);
+  h.mask = mask;
+  return h;
+}
+
+// End of a tile: the lane's span digests; the wave's anchors, from its LDS
+// piece list, to the wave-tile's pool share in position order; the directory
+// entry and the anchor count.  Every lane walks only its own entries (a chain
+// through the list, newest first, `last` = its newest): once to count, once
+// to store, so the list costs O(entries per lane), not O(entries).  Returns a
+// lower bound of the global stores it leaves in flight (the digests, the
+// directory pair, the count) so the next round's wait can leave them be.  A
+// wave-tile whose list or pool share overflowed is marked for the exact
+// rescan (zc_anchor_rescan) and stores no anchors.
+template <int ABL>
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
                                                   const uint64_t (&bk)[kDigests], const WaveList& wl,
-                                                  uint64_t* __restrict__ blk, PoolOut po,
+                                                  uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
                                                   unsigned long long* __restrict__ counters) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
 #pragma unroll
@@ -459,123 +493,39 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
                        (uint32_t)(bk[2 * t + 1] >> 32));
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)wt * po.wcap;
-  if (wl.n > ZC_WLIST) {
-    if (lane == 0) {
-      po.cnt[wt] = ZC_WT_OVERFLOW;
-      atomicAdd(&counters[CNT_OVERFLOW], 1ull);
-    }
-    return 0;
-  }
-  // 1) lanes decode the listed pieces in parallel (entry 64 c + lane in
-  //    register c): hit mask (bits 0-15), piece index (16-23), owner lane
-  //    (24-29) and the first hit's gear.  Kept in registers and read back with
-  //    v_readlane: an LDS store here would have to wait for the ring's DMA.
-  constexpr int kChunks = (ZC_WLIST + 63) / 64;
-  uint32_t ent[kChunks], eg[kChunks];
-#pragma unroll
-  for (int c = 0; c < kChunks; ++c) {
-    const uint32_t i = 64 * c + lane;
-    uint32_t e0 = 0, g = 0, g1 = 0, mask = 0;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (i < wl.n) {
-      e0 = wl.e[2 * i];
-      g = wl.e[2 * i + 1];
-      v = wl.x[i];
-    }
-    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        g = (g << 1) + ((xs[d] >> (8 * k)) & 0xFFu);
-        const bool hit = (int32_t)g >= lo_thr;
-        g1 = (hit && !mask) ? g : g1;
-        mask |= hit ? 1u << (4 * d + k) : 0u;
-      }
-    ent[c] = ((e0 >> 16) << 24) | (((e0 & 0xFFFFu) >> 4) << 16) | mask;
-    eg[c] = g1;
-  }
-  // 2) every lane collects its own anchors, in position order, in registers
-  //    (offsets below 63 of the stream are no anchors)
-  uint32_t cnt = 0, rr[kTileSlots], gg[kTileSlots];
-#pragma unroll
-  for (int t = 0; t < kTileSlots; ++t) rr[t] = gg[t] = 0;
-  auto push = [&](bool mine, uint32_t rel, uint32_t g) {
-    mine = mine && span0 + rel >= ZC_ANCHOR_MIN_OFF;
-#pragma unroll
-    for (int t = 0; t < kTileSlots; ++t) {
-      rr[t] = (mine && cnt == (uint32_t)t) ? rel : rr[t];
-      gg[t] = (mine && cnt == (uint32_t)t) ? g : gg[t];
-    }
-    cnt += mine ? 1u : 0u;
-  };
-  // the further anchors of a piece (rare), the gear rolled on from the first
-  auto more = [&](uint32_t i, bool mine, uint32_t mask, uint32_t p16, uint32_t t1, uint32_t g1, auto&& sink) {
-    const uint4 v = wl.x[i];
-    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-    uint32_t g = g1;
-    for (uint32_t t = t1 + 1; t < 16; ++t) {
-      g = (g << 1) + ((xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
-      sink(mine && ((mask >> t) & 1), p16 + t, g);
-    }
-  };
-  // every listed entry in order: sink(...) for its anchors owned by `who`
-  auto walk = [&](bool who, auto&& sink) {
-#pragma unroll
-    for (int c = 0; c < kChunks; ++c) {
-      const uint32_t m = wl.n > 64u * c ? min(wl.n - 64u * c, 64u) : 0u;
-      for (uint32_t l = 0; l < m; ++l) {
-        const uint32_t e0 = __builtin_amdgcn_readlane(ent[c], l), g1 = __builtin_amdgcn_readlane(eg[c], l);
-        const bool mine = who && (e0 >> 24) == lane;
-        const uint32_t mask = e0 & 0xFFFFu, p16 = ((e0 >> 16) & 0xFFu) << 4;
-        const uint32_t t1 = __builtin_ctz(mask | 0x10000u);
-        sink(mine, p16 + t1, g1);
-        const bool multi = mine && (mask & (mask - 1)) != 0;
-        if (__ballot(multi)) more(64 * c + l, multi, mask, p16, t1, g1, sink);
+  uint32_t tot = 0, excl = 0;
+  bool over = wl.n > ZC_WLIST;
+  if (!over) {
+    uint32_t cnt = 0;
+    for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu)
+      cnt += __popc(piece_hits(wl, i, span0, lo_thr).mask);
+    excl = wave_excl_scan(cnt, lane, &tot);
+    over = tot > po.wcap;
+    if (!over) {
+      // newest entry first: its anchors end at excl + cnt
+      const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
+      uint32_t k = base + excl + cnt;
+      for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
+        const PieceHits h = piece_hits(wl, i, span0, lo_thr);
+        k -= __popc(h.mask);
+        uint32_t g = h.g0, w = k;
+        for (uint32_t t = 0; t < 16; ++t) {
+          g = (g << 1) + ((h.xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+          if ((h.mask >> t) & 1) {
+            po.rel[w] = rbase + h.rel + t;
+            po.g[w] = g;
+            ++w;
+          }
+        }
       }
     }
-  };
-  walk(true, push);
-  uint32_t tot;
-  const uint32_t excl = wave_excl_scan(cnt, lane, &tot);
-  if (tot > po.wcap) {
-    if (lane == 0) {
-      po.cnt[wt] = ZC_WT_OVERFLOW;
-      atomicAdd(&counters[CNT_OVERFLOW], 1ull);
-    }
-    return 0;
-  }
-  const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
-  const bool slow = cnt > (uint32_t)kTileSlots;
-  uint32_t nstores = kDigests / 2;  // the digests
-  // 3) the common case's pool stores: one instruction pair per slot level
-  //    some lane reaches
-#pragma unroll
-  for (int t = 0; t < kTileSlots; ++t) {
-    const bool st = !slow && cnt > (uint32_t)t;
-    if (__ballot(st)) nstores += 2;
-    if (st) {
-      po.rel[base + excl + t] = rbase + rr[t];
-      po.g[base + excl + t] = gg[t];
-    }
-  }
-  if (__ballot(slow)) {
-    // lanes with many anchors: a second pass over the list, storing directly
-    uint32_t k = base + excl;
-    walk(slow, [&](bool mine, uint32_t rel, uint32_t g) {
-      if (mine && span0 + rel >= ZC_ANCHOR_MIN_OFF) {
-        po.rel[k] = rbase + rel;
-        po.g[k] = g;
-        ++k;
-      }
-    });
   }
   if (lane == 0) {
     po.base[wt] = base;
-    po.cnt[wt] = tot;
-    atomicAdd(&counters[CNT_POOL], (unsigned long long)tot);
+    po.cnt[wt] = over ? ZC_WT_OVERFLOW : tot;
+    atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
   }
-  return nstores + 3;  // + the directory pair and the anchor count
+  return kDigests / 2 + 3;
 }
 
 // The workgroup's rounds form one flat sequence over its tiles (33 per tile:
@@ -622,6 +572,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   for (int t = 0; t < kDigests; ++t) bk[t] = 0;
   uint64_t span0 = 0;
   uint32_t tail_stores = 0;  // global stores the last tile end left in flight
+  uint32_t last = kNoEntry;  // this lane's newest entry in the wave's list
 
 #pragma unroll 1
   for (uint32_t R = 0; R < nR; ++R) {
@@ -641,6 +592,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       span0 = (tile0 + blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
       s = ScanLane{0, 0, 0};
       wl.n = 0;
+      last = kNoEntry;
       if (span0 >= 64) {
         const uint32_t xs[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
@@ -655,31 +607,8 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     for (int p = 0; p < kPieces; ++p) v[p] = *(const uint4*)(row + lane * ZC_ROUND + ((p ^ sw) << 4));
     wait_lgkmcnt<0>();  // the slot is free
     if (R + 2 < nR) issue(R + 2);
-    if (ABL & ABL_DEFER) {
-      // the round's pieces hashed without branches; pieces with anchors are
-      // listed afterwards (their bytes and entry gear are still in registers)
-      uint64_t hm[kPieces];
-      uint32_t g0[kPieces];
 #pragma unroll
-      for (int p = 0; p < kPieces; ++p) {
-        g0[p] = s.glo;
-        scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lane, lo_thr, s, wl, &hm[p]);
-      }
-#pragma unroll
-      for (int p = 0; p < kPieces; ++p)
-        if (hm[p]) {
-          const uint32_t idx = wl.n + lane_prefix(hm[p]);
-          if (((hm[p] >> lane) & 1) && idx < ZC_WLIST) {
-            wl.e[2 * idx] = (lane << 16) | ((uint32_t)r * ZC_ROUND + p * 16);
-            wl.e[2 * idx + 1] = g0[p];
-            wl.x[idx] = v[p];
-          }
-          wl.n += __popcll(hm[p]);
-        }
-    } else {
-#pragma unroll
-      for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lane, lo_thr, s, wl);
-    }
+    for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lo_thr, s, wl, last);
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const int q = r / (ZC_SPAN / ZC_ROUND);
@@ -689,7 +618,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       s.hlo = s.hhi = 0;
     }
     if (r == kRounds - 1 && !(ABL & ABL_NO_TILE_END))
-      tail_stores = scan_tile_end(span0, lane, lo_thr, bk, wl, blk, po, counters);
+      tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, counters);
   }
 }
 
