@@ -57,6 +57,29 @@ def cpu_baseline(sample_bytes, seed):
             "chunks_per_s": round(len(recs) / dt, 1)}
 
 
+def rank_seed(base, rank):
+    """Replica streams are independent: rank r chunks the stream seeded base + r
+    (BASELINE.json configs[3]: one 8 GiB buffer per GPU, seed = base + gpu)."""
+    return base + rank
+
+
+def job_elapsed(elapsed, world):
+    """Whole-job time of the timed region = the max over ranks (each rank
+    brackets its own steps with a barrier and a device sync)."""
+    if world <= 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_value(n_bytes_per_rank, world, steps, elapsed):
+    """Aggregate GiB/s: the bytes every rank chunked over the job time."""
+    return n_bytes_per_rank * world * steps / elapsed / 2**30
+
+
 def pmc_traffic(n_bytes):
     """HBM bytes per zc_scan launch from the committed rocprofv3 --pmc summary
     (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE), if present."""
@@ -90,7 +113,7 @@ def main():
 
     n = int(args.gib * 2**30)
     buf = torch.empty(n, dtype=torch.uint8, device=f"cuda:{local}")
-    seed = args.seed + rank
+    seed = rank_seed(args.seed, rank)
     if args.config == "c5":
         buf.zero_()
     elif args.config == "c3":
@@ -119,13 +142,9 @@ def main():
     elapsed = time.perf_counter() - t0
     st = bc.stats()
     nrec = len(bc.records())
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = job_elapsed(elapsed, world)
     ms_step = elapsed / args.steps * 1e3
-    total_bytes = n * world * args.steps
-    value = total_bytes / elapsed / 2**30
+    value = job_value(n, world, args.steps, elapsed)
 
     e2e = None
     if args.e2e:

@@ -25,6 +25,9 @@ int main(int argc, char** argv) {
   struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
   std::vector<V> vs = {
     {"full", zc_scan_kernel<0>, {}},
+    {"full_no_atomic", zc_scan_kernel<ABL_NO_ATOMIC>, {}},
+    {"stage_only_no_atomic", zc_scan_kernel<ABL_NO_BYTES | ABL_NO_ATOMIC>, {}},
+    {"no_digest_no_atomic", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_ATOMIC>, {}},
     {"no_record", zc_scan_kernel<ABL_NO_RECORD>, {}},
     {"no_digest", zc_scan_kernel<ABL_NO_DIGEST>, {}},
     {"no_digest_no_record", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_RECORD>, {}},

@@ -179,7 +179,7 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 // 32 = anchor threshold raised so the recording block is (almost) never taken,
 // 64 = no tile-end work (span digests, anchors to the pool)
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32, ABL_NO_TILE_END = 64 };
+       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128 };
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
   uint32_t* e;      // {(rel of the piece >> 4) << 8 | the lane's previous entry, gear before the piece}
@@ -523,7 +523,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   if (lane == 0) {
     po.base[wt] = base;
     po.cnt[wt] = over ? ZC_WT_OVERFLOW : tot;
-    atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
+    if (!(ABL & ABL_NO_ATOMIC)) atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
   }
   return kDigests / 2 + 3;
 }
