@@ -51,7 +51,9 @@ enum {
   ZC_FLAG_SHA1 = 1u,     /* compute the SHA-1 half of every chunk id (ChunkId::cryptoHash)
                             and register the stream's new chunks in the context's index,
                             so a later stream on the same context can match them */
-  ZC_FLAG_TIMING = 2u    /* record per-stage device timings (zc_get_stats) */
+  ZC_FLAG_TIMING = 2u,   /* record per-stage device timings (zc_get_stats) */
+  ZC_FLAG_NO_STAGED_SCREEN = 4u  /* diagnostics: run the exact-hash screen on its lane-per-KiB
+                                    kernel only (same records, slower; tests cover both) */
 };
 
 /* record kinds: chunk_to_emit of a chunk cut and saved by this stream (NEW),

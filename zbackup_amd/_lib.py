@@ -10,7 +10,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libzchunk.so")
 
 ZC_OK, ZC_ERR_ARG, ZC_ERR_HIP, ZC_ERR_NOMEM, ZC_ERR_STATE = 0, -1, -2, -3, -4
-ZC_FLAG_SHA1, ZC_FLAG_TIMING = 1, 2
+ZC_FLAG_SHA1, ZC_FLAG_TIMING, ZC_FLAG_NO_STAGED_SCREEN = 1, 2, 4
 ZC_CHUNK_NEW, ZC_CHUNK_DUP, ZC_BYTES = 0, 1, 2
 
 # every symbol include/zchunk.h declares

@@ -57,10 +57,12 @@ class BackupCreator:
     """One stream through the engine.  `seeds` are (sha1_16, rolling, size)
     entries of an existing index (ChunkIndex::loadIndex)."""
 
-    def __init__(self, chunk_max_size=65536, seeds=(), device=0, sha1=True, timing=False):
+    def __init__(self, chunk_max_size=65536, seeds=(), device=0, sha1=True, timing=False, staged_screen=True):
         self._L = _lib.load()
         self.chunk_max_size = int(chunk_max_size)
         flags = (_lib.ZC_FLAG_SHA1 if sha1 else 0) | (_lib.ZC_FLAG_TIMING if timing else 0)
+        if not staged_screen:  # diagnostics: the lane-per-KiB exact screen only
+            flags |= _lib.ZC_FLAG_NO_STAGED_SCREEN
         ctx = ctypes.c_void_p()
         rc = self._L.zc_create(ctypes.byref(ctx), self.chunk_max_size, device, flags)
         if rc != _lib.ZC_OK:

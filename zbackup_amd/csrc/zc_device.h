@@ -46,6 +46,15 @@ constexpr int ZC_WT_BLOCK = (1 << ZC_WT_SHIFT) / ZC_SPAN;
 // zc_fscan: lane span 1 KiB, 256 KiB per workgroup
 constexpr uint64_t ZC_TILE = (uint64_t)ZC_SPAN * ZC_TPB;
 constexpr int ZC_RUN_SLOTS = 4;                              // LDS screen-run slots per lane
+// zc_fscan_staged: one wave per screen wave-tile of 64 lane spans of
+// ZC_FLSPAN bytes (512 KiB), in-bytes and out-bytes (p - W) staged through
+// LDS in ZC_FROUND-byte rounds; 8 waves per workgroup, persistent
+constexpr int ZC_FLSPAN = 8192;
+constexpr int ZC_FROUND = 64;
+constexpr int ZC_FTPB = 512;
+constexpr uint64_t ZC_FWT = 64ull * ZC_FLSPAN;
+static_assert(ZC_FWT % ZC_TILE == 0, "screen wave-tiles cover whole zc_fscan tiles");
+constexpr uint32_t ZC_FWT_OVERFLOW = 0xFFFFFFFFu;            // wave-tile left for zc_fscan
 
 // Content anchors.  gear(q) = sum_{j<32} b[q-j] * 2^j (mod 2^32); q is an
 // anchor iff (int32)gear(q) >= anchor_lo, i.e. gear in [anchor_lo, 0x7FFFFFFF]:
@@ -164,10 +173,23 @@ hipError_t launch_range_digest(const uint8_t* data, uint64_t n, const uint64_t* 
                                const uint64_t* a, const uint64_t* b, uint32_t nr, uint64_t* out,
                                hipStream_t s);
 
+// exact screen, lane per 1 KiB: zc_fscan tiles [tile0, tile0 + ntiles) of
+// ZC_TILE bytes, positions p in [p_start, p_end); runs of tile t at
+// runs[tile_off[t] ...], tile_cnt[t] of them (merged inside the tile)
 hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W,
-                        uint32_t pw32, uint64_t p_start, const uint32_t* f32, uint32_t nf,
-                        const uint32_t* fbits, Run* runs, uint64_t runs_cap, uint64_t* tile_off, uint32_t* tile_cnt,
-                        unsigned long long* counters, hipStream_t s);
+                        uint32_t pw32, uint64_t p_start, uint64_t p_end, uint64_t tile0, uint64_t ntiles,
+                        const uint32_t* f32, uint32_t nf, const uint32_t* fbits, Run* runs, uint64_t runs_cap,
+                        uint64_t* tile_off, uint32_t* tile_cnt, unsigned long long* counters, hipStream_t s);
+
+// exact screen, staged: screen wave-tiles [wt0, wt0 + nwt) of ZC_FWT bytes
+// (all inside the stream, wt0 * ZC_FWT >= W + 16, W >= 32); keys: nf <= 4
+// compared directly, else the 2^17-bit map fbits17 (bit (h >> 15));
+// wt_cnt[wt] = ZC_FWT_OVERFLOW marks a wave-tile whose runs did not fit (to
+// be redone by launch_fscan)
+hipError_t launch_fscan_staged(const uint8_t* data, const uint64_t* blk, uint32_t W, uint32_t pw32,
+                               uint64_t p_start, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
+                               uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
+                               uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_sha1(const uint8_t* data, const uint64_t* a, const uint32_t* len, uint32_t nr,
                        uint8_t* out20, hipStream_t s);

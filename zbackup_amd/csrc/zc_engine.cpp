@@ -163,7 +163,9 @@ struct zc_ctx {
   DevBuf<uint64_t> va, vb, dout;
   DevBuf<uint32_t> vlen;
   DevBuf<uint8_t> vok, sha_out;
-  DevBuf<uint32_t> f32, fbits;
+  DevBuf<uint32_t> f32, fbits, fbits17;
+  DevBuf<uint64_t> fwt_off;
+  DevBuf<uint32_t> fwt_cnt;
   DevBuf<Run> runs;
   DevBuf<uint32_t> ancless;
   HostBuf<unsigned long long> h_cnt;
@@ -630,16 +632,57 @@ class Resolver {
     }
     const uint64_t p_start = r_e_ + W_ - 1;
     if (p_start >= n_) return;
+    const uint32_t pw32 = (uint32_t)pow257(W_);
     const uint64_t ntiles = (n_ + ZC_TILE - 1) / ZC_TILE;
+    // screen wave-tiles [wt_lo, wt_hi) go through the staged kernel (whole
+    // wave-tiles inside the stream, out-bytes of every lane in range); the
+    // head before them and the tail after them through zc_fscan
+    const uint64_t t_first = p_start / ZC_TILE;
+    uint64_t wt_lo = std::max<uint64_t>(((uint64_t)W_ + 16 + ZC_FWT - 1) / ZC_FWT, p_start / ZC_FWT);
+    uint64_t wt_hi = n_ / ZC_FWT;
+    const bool staged = W_ >= 32 && wt_hi > wt_lo && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN);
+    if (!staged) wt_lo = wt_hi = 0;
+    constexpr uint64_t kTpw = ZC_FWT / ZC_TILE;  // zc_fscan tiles per screen wave-tile
+    const uint64_t head_end = staged ? wt_lo * kTpw : ntiles;  // zc_fscan tiles [t_first, head_end)
+    const uint64_t tail_beg = staged ? wt_hi * kTpw : ntiles;  // ... and [tail_beg, ntiles)
     c_.ftile_off.ensure(ntiles);
     c_.ftile_cnt.ensure(ntiles);
+    c_.fwt_off.ensure(std::max<uint64_t>(wt_hi, 1));
+    c_.fwt_cnt.ensure(std::max<uint64_t>(wt_hi, 1));
+    if (staged && nf > 4) {
+      std::vector<uint32_t> map17(1u << 12, 0);
+      for (uint32_t h : keys32) map17[(h >> 15) >> 5] |= 1u << ((h >> 15) & 31);
+      c_.fbits17.ensure(map17.size());
+      h2d(c_, c_.fbits17.p, map17.data(), map17.size());
+    }
     uint64_t cap = std::max<uint64_t>(ntiles * 4, 1u << 16);
     unsigned long long cnt[CNT_LAST];
+    std::vector<uint64_t> wt_over;
+    auto old_screen = [&](uint64_t t0, uint64_t t1, uint64_t p_end) {
+      if (t1 > t0)
+        HCK(launch_fscan(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
+                         c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
+    };
+    std::vector<uint32_t> wcnt(wt_hi > wt_lo ? wt_hi - wt_lo : 0);
     for (int attempt = 0; attempt < 3; ++attempt) {
       c_.runs.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
-      HCK(launch_fscan(d_, n_, c_.blk.p, W_, (uint32_t)pow257(W_), p_start, c_.f32.p, nf, c_.fbits.p,
-                       c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
+      old_screen(t_first, head_end, staged ? wt_lo * ZC_FWT : n_);
+      if (staged) {
+        HCK(launch_fscan_staged(d_, c_.blk.p, W_, pw32, p_start, wt_lo, wt_hi - wt_lo, keys32.data(), nf,
+                                c_.fbits17.p, c_.runs.p, c_.runs.cap, c_.fwt_off.p, c_.fwt_cnt.p, c_.counters.p,
+                                c_.stream));
+        old_screen(std::max(tail_beg, t_first), ntiles, n_);
+        d2h(c_, wcnt.data(), c_.fwt_cnt.p + wt_lo, wcnt.size());
+        sync(c_);
+        // wave-tiles whose runs overflowed the lane slots: redo with zc_fscan
+        wt_over.clear();
+        for (uint64_t i = 0; i < wcnt.size(); ++i)
+          if (wcnt[i] == ZC_FWT_OVERFLOW) {
+            wt_over.push_back(wt_lo + i);
+            old_screen((wt_lo + i) * kTpw, (wt_lo + i + 1) * kTpw, (wt_lo + i + 1) * ZC_FWT);
+          }
+      }
       d2h(c_, cnt, c_.counters.p, CNT_LAST);
       sync(c_);
       if (!cnt[CNT_FOVF]) break;
@@ -649,20 +692,32 @@ class Resolver {
     const uint64_t nruns = cnt[CNT_RUNS];
     c_.stats.fscan_runs += nruns;
     std::vector<Run> raw(nruns);
-    std::vector<uint64_t> toff(ntiles);
+    std::vector<uint64_t> toff(ntiles), woff(wcnt.size());
     std::vector<uint32_t> tcnt(ntiles);
     d2h(c_, raw.data(), c_.runs.p, nruns);
     d2h(c_, toff.data(), c_.ftile_off.p, ntiles);
     d2h(c_, tcnt.data(), c_.ftile_cnt.p, ntiles);
+    d2h(c_, woff.data(), c_.fwt_off.p + wt_lo, woff.size());
     sync(c_);
-    for (uint64_t t = 0; t < ntiles; ++t)
-      for (uint32_t i = 0; i < tcnt[t]; ++i) {
-        const Run& q = raw[toff[t] + i];
-        if (!runs_.empty() && runs_.back().end == q.start)
-          runs_.back().end = q.end;
+    auto take = [&](const Run* q, uint64_t k) {
+      for (uint64_t i = 0; i < k; ++i) {
+        if (!runs_.empty() && runs_.back().end == q[i].start)
+          runs_.back().end = q[i].end;
         else
-          runs_.push_back(q);
+          runs_.push_back(q[i]);
       }
+    };
+    auto take_tiles = [&](uint64_t t0, uint64_t t1) {
+      for (uint64_t t = t0; t < t1; ++t) take(&raw[toff[t]], tcnt[t]);
+    };
+    take_tiles(t_first, head_end);
+    for (uint64_t i = 0; i < wcnt.size(); ++i) {
+      if (wcnt[i] == ZC_FWT_OVERFLOW)
+        take_tiles((wt_lo + i) * kTpw, (wt_lo + i + 1) * kTpw);
+      else
+        take(&raw[woff[i]], wcnt[i]);
+    }
+    take_tiles(std::max(tail_beg, t_first), ntiles);
     has_f_ = !runs_.empty();
   }
 

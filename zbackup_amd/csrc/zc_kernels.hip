@@ -932,7 +932,7 @@ constexpr uint32_t kFBitmapWords = 1u << 14;  // 2^19 bits = 64 KiB, index = h >
 
 __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, const uint64_t* __restrict__ blk, uint32_t W,
-    uint32_t pw32, uint64_t p_start, const uint32_t* __restrict__ f32, uint32_t nf,
+    uint32_t pw32, uint64_t p_start, uint64_t p_end, uint64_t tile0, const uint32_t* __restrict__ f32, uint32_t nf,
     const uint32_t* __restrict__ fbits, Run* __restrict__ runs, uint64_t runs_cap,
     uint64_t* __restrict__ tile_off, uint32_t* __restrict__ tile_cnt,
     unsigned long long* __restrict__ counters) {
@@ -943,7 +943,7 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
   __shared__ uint32_t s_keys[kFLinearMax];
 
   const uint32_t tid = threadIdx.x;
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = tile0 + blockIdx.x;
   const uint32_t* s_bits = nullptr;
   if (nf > kFLinearMax) {
     for (uint32_t i = tid; i < kFBitmapWords; i += ZC_TPB) s_dyn[i] = fbits[i];
@@ -955,7 +955,8 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
 
   const uint64_t span0 = tile * ZC_TILE + (uint64_t)tid * ZC_SPAN;
   uint64_t ps = span0 > p_start ? span0 : p_start;
-  uint64_t pe = span0 + ZC_SPAN < n ? span0 + ZC_SPAN : n;
+  const uint64_t lim = p_end < n ? p_end : n;
+  uint64_t pe = span0 + ZC_SPAN < lim ? span0 + ZC_SPAN : lim;
   uint32_t cnt = 0;
   uint64_t open = ~0ull;
   auto emit = [&](uint64_t a, uint64_t b) {
@@ -1092,6 +1093,286 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
     }
     bool last = (i + 1 == total) || (s_re[i] != s_rs[i + 1]);
     if (last) runs[base + hid - 1].end = s_re[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// zc_fscan_staged: the same exact screen at streaming speed.
+//
+// One wave per screen wave-tile (64 lane spans of ZC_FLSPAN bytes, a lane
+// rolls H(p) mod 2^32 through its span), persistent over the wave-tiles.  Both
+// byte streams a lane needs -- the in-bytes b[p] and the out-bytes b[p - W] --
+// are staged through a private 2-slot LDS ring with global_load_lds_dwordx4,
+// 64-byte rounds, rows 8 KiB apart (tools/ubench/stage_bench2.hip: 4 KiB row
+// strides lose ~12 % of the streaming rate, 8 KiB ones do not).  The out-rows
+// are staged 16-byte aligned one piece ahead of the bytes they serve; a lane
+// keeps the previous piece and funnels each 16-byte out piece from two staged
+// ones (the misalignment m = -W mod 16 is kernel-uniform: Q = m >> 2 is a
+// template parameter, m & 3 an alignbyte).
+//
+// Per byte: V = 257 V + b[p] - 257^W b[p-W] (V = H(p) - 257^W); the key test
+// is one compare per key (NF <= 4) or a bit of an LDS map, and its ballot is
+// folded into two wave masks per 16-byte piece (lanes with any hit, lanes with
+// all hits).  Only a lane whose run state changes inside a piece (a run opens
+// or closes, or the piece straddles p_start) re-rolls the piece to record run
+// boundaries, so all-hit and no-hit data (all-zero streams, random streams)
+// pay the roll and the compare only.  Runs are closed at span ends and merged
+// across the wave at the wave-tile end.
+constexpr int kFRounds = ZC_FLSPAN / ZC_FROUND;          // rounds per wave-tile
+constexpr int kFDmaHalf = 64 * ZC_FROUND / 1024;         // DMA instructions per stream per round
+constexpr int kFDma = 2 * kFDmaHalf;
+constexpr int kFPieces = ZC_FROUND / 16;
+constexpr int kFRunSlots = 2;                            // runs per lane per wave-tile (else overflow)
+constexpr uint32_t kFMapWords = 1u << 12;                // 2^17-bit key map, bit (h >> 15)
+__host__ __device__ constexpr uint32_t frow_swizzle(uint32_t row) { return (row / (256 / ZC_FROUND)) % kFPieces; }
+
+struct FKeys {
+  uint32_t k[4];  // keys - 257^W (compared with V); unused slots repeat k[0]
+};
+
+// Rabin-Karp accumulator mod 2^32 of [a, a + W) for a, W multiples of ZC_SPAN:
+// a fold of span digests, loads batched eight at a time
+__device__ __forceinline__ uint32_t fold_spans32(const uint64_t* __restrict__ blk, uint64_t a, uint32_t nspan) {
+  const uint32_t m = (uint32_t)span_mul();
+  uint32_t acc = 0;
+  const uint64_t* p = blk + a / ZC_SPAN;
+  uint32_t k = 0;
+  for (; k + 8 <= nspan; k += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (uint32_t)p[k + i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = acc * m + v[i];
+  }
+  for (; k < nspan; ++k) acc = acc * m + (uint32_t)p[k];
+  return acc;
+}
+
+template <int NF>
+__device__ __forceinline__ bool f_hit(uint32_t V, const FKeys& K, const uint32_t* s_map, uint32_t pw32) {
+  if (NF == 1) return V == K.k[0];
+  if (NF == 4) return (V == K.k[0]) | (V == K.k[1]) | (V == K.k[2]) | (V == K.k[3]);
+  const uint32_t h = (V + pw32) >> 15;
+  return (s_map[h >> 5] >> (h & 31)) & 1u;
+}
+
+// 16-byte window at byte offset 4Q + s of the 32 bytes lo||hi
+template <int Q>
+__device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, uint32_t s) {
+  const uint32_t a[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  return make_uint4(__builtin_amdgcn_alignbyte(a[Q + 1], a[Q], s), __builtin_amdgcn_alignbyte(a[Q + 2], a[Q + 1], s),
+                    __builtin_amdgcn_alignbyte(a[Q + 3], a[Q + 2], s),
+                    __builtin_amdgcn_alignbyte(a[Q + 4], a[Q + 3], s));
+}
+
+template <int Q, int NF>
+__global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk, uint32_t W, uint32_t pw32, uint32_t sbyte,
+    uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* __restrict__ fmap,
+    Run* __restrict__ runs, uint64_t runs_cap, uint64_t* __restrict__ wt_off, uint32_t* __restrict__ wt_cnt,
+    unsigned long long* __restrict__ counters) {
+  constexpr int kWaves = ZC_FTPB / 64;
+  constexpr uint32_t kSlot = 64 * ZC_FROUND;  // bytes of one stream's round
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves][2][2 * kSlot];  // [slot][in | out]
+  __shared__ uint32_t s_map[NF == 0 ? kFMapWords : 1];
+  __shared__ uint32_t s_rs[kWaves][64 * kFRunSlots], s_re[kWaves][64 * kFRunSlots];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (NF == 0) {
+    for (uint32_t i = tid; i < kFMapWords; i += ZC_FTPB) s_map[i] = fmap[i];
+    __syncthreads();
+  }
+  const uint32_t m = (uint32_t)(4 * Q) + sbyte;  // = -W mod 16
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave, nw = (uint64_t)gridDim.x * kWaves;
+  const uint32_t ntk = nwt > gw ? (uint32_t)((nwt - 1 - gw) / nw + 1) : 0;
+  const uint32_t nR = ntk * kFRounds;
+  uint8_t* myring = ring[wave][0];
+  uint32_t* lrs = s_rs[wave];
+  uint32_t* lre = s_re[wave];
+  // this lane's share of DMA instruction j (rows 8 KiB apart, source piece
+  // swizzled so the per-lane ds_read_b128 of a row is conflict free)
+  uint32_t lane_off[kFDmaHalf];
+#pragma unroll
+  for (int j = 0; j < kFDmaHalf; ++j) {
+    const uint32_t row = j * (1024 / ZC_FROUND) + lane / kFPieces;
+    lane_off[j] = row * ZC_FLSPAN + ((lane % kFPieces) ^ frow_swizzle(row)) * 16;
+  }
+  const uint32_t sw = frow_swizzle(lane);
+  const uint64_t out_shift = (uint64_t)W + m - 16;  // staged out-row = in-row - out_shift
+  auto issue = [&](uint32_t Rx) {
+    const uint32_t k = Rx / kFRounds, r = Rx - k * kFRounds;
+    const uint64_t wtb = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT + (uint64_t)r * ZC_FROUND;
+    uint8_t* dst = myring + (Rx & 1) * (2 * kSlot);
+#pragma unroll
+    for (int j = 0; j < kFDmaHalf; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wtb + lane_off[j]), (lds_void_t*)(dst + j * 1024), 16, 0,
+                                       0);
+#pragma unroll
+    for (int j = 0; j < kFDmaHalf; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wtb + lane_off[j] - out_shift),
+                                       (lds_void_t*)(dst + kSlot + j * 1024), 16, 0, 0);
+  };
+  if (nR > 0) issue(0);
+  if (nR > 1) issue(1);
+
+  uint32_t V = 0;
+  uint4 carry = make_uint4(0, 0, 0, 0);
+  uint64_t wtbase = 0, ps = 0;
+  bool open = false, ovf = false;
+  uint64_t open_mask = 0;  // wave-uniform mirror of `open`
+  bool need_valid = false;
+  uint32_t rstart = 0, nrun = 0;
+  uint32_t rs[kFRunSlots], re[kFRunSlots];
+
+#pragma unroll 1
+  for (uint32_t R = 0; R < nR; ++R) {
+    const uint32_t k = R / kFRounds, r = R - k * kFRounds;
+    if (r == 0) {
+      // a new wave-tile: drain everything in flight (its first two rounds and
+      // the previous wave-tile's stores), then the lane's start state: V of
+      // the window ending just before the span, and the out-piece before it
+      wait_vmcnt<0>();
+      wtbase = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT;
+      ps = wtbase + (uint64_t)lane * ZC_FLSPAN;
+      const uint64_t a = ps - W;
+      V = (W % ZC_SPAN == 0) ? fold_spans32(blk, a, W / ZC_SPAN) : rk_acc32(data, blk, a, ps);
+      carry = *(const uint4*)(data + ps - W - m);
+      need_valid = wtbase < p_start;
+      open = false;
+      open_mask = 0;
+      ovf = false;
+      nrun = 0;
+    } else if (R + 1 < nR) {
+      wait_vmcnt<kFDma>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    const uint8_t* slot = myring + (R & 1) * (2 * kSlot);
+    uint4 vin[kFPieces], vst[kFPieces];
+#pragma unroll
+    for (int p = 0; p < kFPieces; ++p) {
+      vin[p] = *(const uint4*)(slot + lane * ZC_FROUND + ((p ^ sw) << 4));
+      vst[p] = *(const uint4*)(slot + kSlot + lane * ZC_FROUND + ((p ^ sw) << 4));
+    }
+    wait_lgkmcnt<0>();  // the slot is free
+    if (R + 2 < nR) issue(R + 2);
+
+#pragma unroll
+    for (int p = 0; p < kFPieces; ++p) {
+      const uint4 vout = funnel16<Q>(p == 0 ? carry : vst[p - 1], vst[p], sbyte);
+      const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
+      const uint32_t xout[4] = {vout.x, vout.y, vout.z, vout.w};
+      const uint32_t V0 = V;
+      uint64_t any = 0, all = ~0ull;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          V = V * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - ((xout[d] >> (8 * q)) & 0xFFu) * pw32;
+          const uint64_t b = __ballot(f_hit<NF>(V, K, s_map, pw32));
+          any |= b;
+          all &= b;
+        }
+      uint64_t need = (open_mask & ~all) | (~open_mask & any);
+      const uint64_t pp = ps + (uint64_t)r * ZC_FROUND + 16 * p;  // first position of the piece
+      if (need_valid) {
+        const uint64_t none = __ballot(pp + 16 <= p_start);
+        const uint64_t some = __ballot(pp < p_start);  // at least one position before p_start
+        need = (need & ~some) | (some & ~none & (any | open_mask));
+      }
+      if (__builtin_expect(need != 0, 0)) {
+        if ((need >> lane) & 1) {
+          uint32_t Vx = V0;
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              Vx = Vx * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - ((xout[d] >> (8 * q)) & 0xFFu) * pw32;
+              const uint64_t pos = pp + 4 * d + q;
+              const bool h = f_hit<NF>(Vx, K, s_map, pw32) && pos >= p_start;
+              const uint32_t rel = (uint32_t)(pos - wtbase);
+              if (h && !open) {
+                open = true;
+                rstart = rel;
+              } else if (!h && open) {
+                open = false;
+                if (nrun < kFRunSlots) {
+                  rs[nrun == 0 ? 0 : 1] = rstart;
+                  re[nrun == 0 ? 0 : 1] = rel;
+                } else {
+                  ovf = true;
+                }
+                ++nrun;
+              }
+            }
+        }
+        open_mask = __ballot(open);
+      }
+    }
+    carry = vst[kFPieces - 1];
+
+    if (r == kFRounds - 1) {
+      // wave-tile end: close runs at span ends, merge across lanes, write
+      if (open) {
+        if (nrun < kFRunSlots) {
+          rs[nrun == 0 ? 0 : 1] = rstart;
+          re[nrun == 0 ? 0 : 1] = (lane + 1) * ZC_FLSPAN;
+        } else {
+          ovf = true;
+        }
+        ++nrun;
+        open = false;
+      }
+      const uint64_t wt = wtbase / ZC_FWT;
+      if (__ballot(ovf) != 0) {
+        if (lane == 0) {
+          wt_off[wt] = 0;
+          wt_cnt[wt] = ZC_FWT_OVERFLOW;
+        }
+        continue;
+      }
+      uint32_t tot;
+      const uint32_t excl = wave_excl_scan(nrun, lane, &tot);
+      if (tot == 0) {
+        if (lane == 0) {
+          wt_off[wt] = 0;
+          wt_cnt[wt] = 0;
+        }
+        continue;
+      }
+      for (uint32_t i = 0; i < nrun; ++i) {
+        lrs[excl + i] = rs[i == 0 ? 0 : 1];
+        lre[excl + i] = re[i == 0 ? 0 : 1];
+      }
+      wait_lgkmcnt<0>();
+      __builtin_amdgcn_wave_barrier();
+      // entry i is a head unless it starts where entry i - 1 ends; lane owns
+      // entries lane and lane + 64 (tot <= 128)
+      const uint32_t i0 = lane, i1 = lane + 64;
+      const bool h0 = i0 < tot && (i0 == 0 || lre[i0 - 1] != lrs[i0]);
+      const bool h1 = i1 < tot && lre[i1 - 1] != lrs[i1];
+      const uint64_t hm0 = __ballot(h0), hm1 = __ballot(h1);
+      const uint32_t nh0 = (uint32_t)__popcll(hm0), nheads = nh0 + (uint32_t)__popcll(hm1);
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd(&counters[CNT_RUNS], (unsigned long long)nheads);
+      base = __shfl(base, 0, 64);
+      if (lane == 0) {
+        wt_off[wt] = base;
+        wt_cnt[wt] = nheads;
+        if (base + nheads > runs_cap) atomicOr(&counters[CNT_FOVF], 1ull);
+      }
+      if (base + nheads > runs_cap) continue;
+      // group index of entry i = heads at or before i, minus one
+      const uint32_t g0 = lane_prefix(hm0) + (h0 ? 1u : 0u) - 1u;
+      const uint32_t g1 = nh0 + lane_prefix(hm1) + (h1 ? 1u : 0u) - 1u;
+      if (i0 < tot) {
+        if (h0) runs[base + g0].start = wtbase + lrs[i0];
+        if (i0 + 1 == tot || lre[i0] != lrs[i0 + 1]) runs[base + g0].end = wtbase + lre[i0];
+      }
+      if (i1 < tot) {
+        if (h1) runs[base + g1].start = wtbase + lrs[i1];
+        if (i1 + 1 == tot || lre[i1] != lrs[i1 + 1]) runs[base + g1].end = wtbase + lre[i1];
+      }
+    }
   }
 }
 
@@ -1318,15 +1599,54 @@ hipError_t launch_range_digest(const uint8_t* data, uint64_t n, const uint64_t* 
 }
 
 hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
-                        uint64_t p_start, const uint32_t* f32, uint32_t nf, const uint32_t* fbits,
-                        Run* runs, uint64_t runs_cap, uint64_t* tile_off, uint32_t* tile_cnt,
-                        unsigned long long* counters, hipStream_t s) {
-  uint64_t ntiles = (n + ZC_TILE - 1) / ZC_TILE;
+                        uint64_t p_start, uint64_t p_end, uint64_t tile0, uint64_t ntiles, const uint32_t* f32,
+                        uint32_t nf, const uint32_t* fbits, Run* runs, uint64_t runs_cap, uint64_t* tile_off,
+                        uint32_t* tile_cnt, unsigned long long* counters, hipStream_t s) {
   if (!ntiles) return hipSuccess;
   size_t dyn = nf > kFLinearMax ? kFBitmapWords * sizeof(uint32_t) : 0;
   hipLaunchKernelGGL(zc_fscan_kernel, dim3((unsigned)ntiles), dim3(ZC_TPB), dyn, s, data, n, blk, W, pw32,
-                     p_start, f32, nf, fbits, runs, runs_cap, tile_off, tile_cnt, counters);
+                     p_start, p_end, tile0, f32, nf, fbits, runs, runs_cap, tile_off, tile_cnt, counters);
   return hipGetLastError();
+}
+
+template <int Q>
+static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, const uint8_t* data,
+                                        const uint64_t* blk, uint32_t W, uint32_t pw32, uint32_t sbyte,
+                                        uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* fmap,
+                                        Run* runs, uint64_t runs_cap, uint64_t* wt_off, uint32_t* wt_cnt,
+                                        unsigned long long* counters) {
+#define ZC_FS(NF)                                                                                                  \
+  hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(ZC_FTPB), 0, s, data, blk, W, pw32, sbyte, \
+                     p_start, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
+  if (nfk == 1) ZC_FS(1);
+  else if (nfk == 4) ZC_FS(4);
+  else ZC_FS(0);
+#undef ZC_FS
+  return hipGetLastError();
+}
+
+hipError_t launch_fscan_staged(const uint8_t* data, const uint64_t* blk, uint32_t W, uint32_t pw32,
+                               uint64_t p_start, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
+                               uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
+                               uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
+  if (!nwt) return hipSuccess;
+  if (W < 32 || wt0 * ZC_FWT < (uint64_t)W + 16 || nf == 0) return hipErrorInvalidValue;
+  FKeys K;
+  const int nfk = nf == 1 ? 1 : nf <= 4 ? 4 : 0;
+  for (int i = 0; i < 4; ++i) K.k[i] = (nfk != 0 ? keys32[i < (int)nf ? i : 0] : 0u) - pw32;
+  const uint32_t m = (16u - W % 16u) % 16u;
+  const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * (ZC_FTPB / 64));
+  const unsigned grid = (waves + ZC_FTPB / 64 - 1) / (ZC_FTPB / 64);
+  switch (m >> 2) {
+    case 0: return launch_fscan_staged_q<0>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+                                            runs, runs_cap, wt_off, wt_cnt, counters);
+    case 1: return launch_fscan_staged_q<1>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+                                            runs, runs_cap, wt_off, wt_cnt, counters);
+    case 2: return launch_fscan_staged_q<2>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+                                            runs, runs_cap, wt_off, wt_cnt, counters);
+    default: return launch_fscan_staged_q<3>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K,
+                                             fbits17, runs, runs_cap, wt_off, wt_cnt, counters);
+  }
 }
 
 hipError_t launch_sha1(const uint8_t* data, const uint64_t* a, const uint32_t* len, uint32_t nr,
