@@ -181,12 +181,13 @@ hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, ui
                         const uint32_t* f32, uint32_t nf, const uint32_t* fbits, Run* runs, uint64_t runs_cap,
                         uint64_t* tile_off, uint32_t* tile_cnt, unsigned long long* counters, hipStream_t s);
 
-// exact screen, staged: screen wave-tiles [wt0, wt0 + nwt) of ZC_FWT bytes
-// (all inside the stream, wt0 * ZC_FWT >= W + 16, W >= 32); keys: nf <= 4
-// compared directly, else the 2^17-bit map fbits17 (bit (h >> 15));
-// wt_cnt[wt] = ZC_FWT_OVERFLOW marks a wave-tile whose runs did not fit (to
-// be redone by launch_fscan)
-hipError_t launch_fscan_staged(const uint8_t* data, const uint64_t* blk, uint32_t W, uint32_t pw32,
+// exact screen, staged: screen wave-tiles [wt0, wt0 + nwt) of ZC_FWT bytes,
+// each starting inside the stream (W >= 32, n >= 64), positions p in
+// [p_start, n); keys32 (host memory): nf <= 4 compared directly, else the
+// 2^17-bit map fbits17 (device, bit (h >> 15)); wt_cnt[wt] =
+// ZC_FWT_OVERFLOW marks a wave-tile whose runs did not fit (to be redone by
+// launch_fscan)
+hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                                uint64_t p_start, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
                                uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
                                uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s);

@@ -634,17 +634,14 @@ class Resolver {
     if (p_start >= n_) return;
     const uint32_t pw32 = (uint32_t)pow257(W_);
     const uint64_t ntiles = (n_ + ZC_TILE - 1) / ZC_TILE;
-    // screen wave-tiles [wt_lo, wt_hi) go through the staged kernel (whole
-    // wave-tiles inside the stream, out-bytes of every lane in range); the
-    // head before them and the tail after them through zc_fscan
+    // the staged kernel screens wave-tiles [wt_lo, wt_hi) (the whole range
+    // from p_start to the end); zc_fscan redoes wave-tiles whose runs
+    // overflowed, or everything when the staged kernel does not apply
     const uint64_t t_first = p_start / ZC_TILE;
-    uint64_t wt_lo = std::max<uint64_t>(((uint64_t)W_ + 16 + ZC_FWT - 1) / ZC_FWT, p_start / ZC_FWT);
-    uint64_t wt_hi = n_ / ZC_FWT;
-    const bool staged = W_ >= 32 && wt_hi > wt_lo && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN);
-    if (!staged) wt_lo = wt_hi = 0;
+    const bool staged = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN);
+    const uint64_t wt_lo = staged ? p_start / ZC_FWT : 0;
+    const uint64_t wt_hi = staged ? (n_ + ZC_FWT - 1) / ZC_FWT : 0;
     constexpr uint64_t kTpw = ZC_FWT / ZC_TILE;  // zc_fscan tiles per screen wave-tile
-    const uint64_t head_end = staged ? wt_lo * kTpw : ntiles;  // zc_fscan tiles [t_first, head_end)
-    const uint64_t tail_beg = staged ? wt_hi * kTpw : ntiles;  // ... and [tail_beg, ntiles)
     c_.ftile_off.ensure(ntiles);
     c_.ftile_cnt.ensure(ntiles);
     c_.fwt_off.ensure(std::max<uint64_t>(wt_hi, 1));
@@ -657,31 +654,28 @@ class Resolver {
     }
     uint64_t cap = std::max<uint64_t>(ntiles * 4, 1u << 16);
     unsigned long long cnt[CNT_LAST];
-    std::vector<uint64_t> wt_over;
-    auto old_screen = [&](uint64_t t0, uint64_t t1, uint64_t p_end) {
+    auto old_screen = [&](uint64_t t0, uint64_t t1) {
+      t0 = std::max(t0, t_first);
+      t1 = std::min(t1, ntiles);
       if (t1 > t0)
-        HCK(launch_fscan(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
+        HCK(launch_fscan(d_, n_, c_.blk.p, W_, pw32, p_start, n_, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
                          c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
     };
-    std::vector<uint32_t> wcnt(wt_hi > wt_lo ? wt_hi - wt_lo : 0);
+    std::vector<uint32_t> wcnt(wt_hi - wt_lo);
     for (int attempt = 0; attempt < 3; ++attempt) {
       c_.runs.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
-      old_screen(t_first, head_end, staged ? wt_lo * ZC_FWT : n_);
       if (staged) {
-        HCK(launch_fscan_staged(d_, c_.blk.p, W_, pw32, p_start, wt_lo, wt_hi - wt_lo, keys32.data(), nf,
+        HCK(launch_fscan_staged(d_, n_, c_.blk.p, W_, pw32, p_start, wt_lo, wt_hi - wt_lo, keys32.data(), nf,
                                 c_.fbits17.p, c_.runs.p, c_.runs.cap, c_.fwt_off.p, c_.fwt_cnt.p, c_.counters.p,
                                 c_.stream));
-        old_screen(std::max(tail_beg, t_first), ntiles, n_);
         d2h(c_, wcnt.data(), c_.fwt_cnt.p + wt_lo, wcnt.size());
         sync(c_);
         // wave-tiles whose runs overflowed the lane slots: redo with zc_fscan
-        wt_over.clear();
         for (uint64_t i = 0; i < wcnt.size(); ++i)
-          if (wcnt[i] == ZC_FWT_OVERFLOW) {
-            wt_over.push_back(wt_lo + i);
-            old_screen((wt_lo + i) * kTpw, (wt_lo + i + 1) * kTpw, (wt_lo + i + 1) * ZC_FWT);
-          }
+          if (wcnt[i] == ZC_FWT_OVERFLOW) old_screen((wt_lo + i) * kTpw, (wt_lo + i + 1) * kTpw);
+      } else {
+        old_screen(t_first, ntiles);
       }
       d2h(c_, cnt, c_.counters.p, CNT_LAST);
       sync(c_);
@@ -708,16 +702,15 @@ class Resolver {
       }
     };
     auto take_tiles = [&](uint64_t t0, uint64_t t1) {
-      for (uint64_t t = t0; t < t1; ++t) take(&raw[toff[t]], tcnt[t]);
+      for (uint64_t t = std::max(t0, t_first); t < std::min(t1, ntiles); ++t) take(&raw[toff[t]], tcnt[t]);
     };
-    take_tiles(t_first, head_end);
+    if (!staged) take_tiles(t_first, ntiles);
     for (uint64_t i = 0; i < wcnt.size(); ++i) {
       if (wcnt[i] == ZC_FWT_OVERFLOW)
         take_tiles((wt_lo + i) * kTpw, (wt_lo + i + 1) * kTpw);
       else
         take(&raw[woff[i]], wcnt[i]);
     }
-    take_tiles(std::max(tail_beg, t_first), ntiles);
     has_f_ = !runs_.empty();
   }
 
@@ -727,6 +720,18 @@ class Resolver {
     while (irun_ < runs_.size() && runs_[irun_].end <= from) ++irun_;
     if (irun_ == runs_.size()) return kInf;
     return std::max(from, runs_[irun_].start);
+  }
+
+  // is window [ws, ws + W) known to equal ref without reading it?  It is when
+  // the window is a grid chunk of this epoch in ref's content class (classes
+  // are byte-verified on the device)
+  bool known_equal(uint64_t ws, uint32_t ref) const {
+    if (!indexable_ || ws < r_e_ || (ws - r_e_) % W_) return false;
+    const uint64_t j = (ws - r_e_) / W_;
+    if (j >= nspec_) return false;
+    const uint32_t g = nconf_ + (uint32_t)j;
+    if (g == ref) return true;
+    return !cls_.empty() && cls_[g] == cls_[ref];
   }
 
   // first alive ref with key h visible at p (start order; vis grows with start)
@@ -785,9 +790,13 @@ class Resolver {
       int64_t ref = first_alive_ref(b.h[i], b.pos[i]);
       if (ref >= 0) {
         b.vref[i] = ref;
-        wa.push_back(a[i]);
-        ra.push_back(ref_start(ref));
-        widx.push_back(i);
+        if (known_equal(a[i], (uint32_t)ref)) {
+          b.vok[i] = 1;
+        } else {
+          wa.push_back(a[i]);
+          ra.push_back(ref_start(ref));
+          widx.push_back(i);
+        }
       }
       if (smap_.count(b.h[i])) {
         sa.push_back(a[i]);
@@ -821,6 +830,8 @@ class Resolver {
         bool ok;
         if (fb_.vref[i] == (int64_t)ref) {
           ok = fb_.vok[i];
+        } else if (known_equal(p - W_ + 1, ref)) {
+          ok = true;
         } else {
           std::vector<uint64_t> wa{p - W_ + 1}, ra{ref_start(ref)};
           ok = verify_pairs(wa, ra, W_)[0];

@@ -864,6 +864,11 @@ __global__ void zc_class_insert_kernel(const uint64_t* __restrict__ key, uint32_
                                        uint32_t* cvals, uint32_t cbits) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nref) return;
+  // a ref with the same key as the ref before it is not the lowest of its
+  // key: only the first ref of each run of equal keys inserts (repeated
+  // content -- all-zero streams -- would otherwise serialise every ref on
+  // one slot's atomics)
+  if (i > 0 && key[i - 1] == key[i]) return;
   const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
   const uint32_t mask = (1u << cbits) - 1;
   for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
@@ -1167,8 +1172,8 @@ __device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, uint32_t s) {
 
 template <int Q, int NF>
 __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk, uint32_t W, uint32_t pw32, uint32_t sbyte,
-    uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* __restrict__ fmap,
+    const uint8_t* __restrict__ data, uint64_t n, const uint64_t* __restrict__ blk, uint32_t W, uint32_t pw32,
+    uint32_t sbyte, uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* __restrict__ fmap,
     Run* __restrict__ runs, uint64_t runs_cap, uint64_t* __restrict__ wt_off, uint32_t* __restrict__ wt_cnt,
     unsigned long long* __restrict__ counters) {
   constexpr int kWaves = ZC_FTPB / 64;
@@ -1198,18 +1203,32 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
   }
   const uint32_t sw = frow_swizzle(lane);
   const uint64_t out_shift = (uint64_t)W + m - 16;  // staged out-row = in-row - out_shift
+  // the stream's first and last wave-tiles: source pieces before the stream
+  // or past its end are read from a valid piece instead (their bytes are
+  // never used: out-bytes before the stream count as zero, positions past
+  // the end are not screened)
+  const uint64_t last16 = (n - 16) & ~15ull;
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kFRounds, r = Rx - k * kFRounds;
-    const uint64_t wtb = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT + (uint64_t)r * ZC_FROUND;
+    const uint64_t wtile = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT;
+    const uint64_t wtb = wtile + (uint64_t)r * ZC_FROUND;
+    const bool edge = wtile < out_shift + ZC_FWT || wtile + ZC_FWT > n;
     uint8_t* dst = myring + (Rx & 1) * (2 * kSlot);
 #pragma unroll
-    for (int j = 0; j < kFDmaHalf; ++j)
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wtb + lane_off[j]), (lds_void_t*)(dst + j * 1024), 16, 0,
-                                       0);
+    for (int j = 0; j < kFDmaHalf; ++j) {
+      uint64_t a = wtb + lane_off[j];
+      if (edge && a > last16) a = last16;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + a), (lds_void_t*)(dst + j * 1024), 16, 0, 0);
+    }
 #pragma unroll
-    for (int j = 0; j < kFDmaHalf; ++j)
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wtb + lane_off[j] - out_shift),
-                                       (lds_void_t*)(dst + kSlot + j * 1024), 16, 0, 0);
+    for (int j = 0; j < kFDmaHalf; ++j) {
+      uint64_t a = wtb + lane_off[j] - out_shift;
+      if (edge) {
+        const uint64_t in = wtb + lane_off[j];
+        a = in < out_shift ? 0 : (a > last16 ? last16 : a);
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + a), (lds_void_t*)(dst + kSlot + j * 1024), 16, 0, 0);
+    }
   };
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
@@ -1219,7 +1238,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
   uint64_t wtbase = 0, ps = 0;
   bool open = false, ovf = false;
   uint64_t open_mask = 0;  // wave-uniform mirror of `open`
-  bool need_valid = false;
+  bool need_valid = false, head = false;
   uint32_t rstart = 0, nrun = 0;
   uint32_t rs[kFRunSlots], re[kFRunSlots];
 
@@ -1233,10 +1252,27 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
       wait_vmcnt<0>();
       wtbase = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT;
       ps = wtbase + (uint64_t)lane * ZC_FLSPAN;
-      const uint64_t a = ps - W;
-      V = (W % ZC_SPAN == 0) ? fold_spans32(blk, a, W / ZC_SPAN) : rk_acc32(data, blk, a, ps);
-      carry = *(const uint4*)(data + ps - W - m);
-      need_valid = wtbase < p_start;
+      // (bytes before the stream count as zero: V(p) = acc of [max(0, p - W + 1), p])
+      V = 0;
+      carry = make_uint4(0, 0, 0, 0);
+      if (ps < n) {
+        if (ps >= W)
+          V = (W % ZC_SPAN == 0) ? fold_spans32(blk, ps - W, W / ZC_SPAN) : rk_acc32(data, blk, ps - W, ps);
+        else
+          V = fold_spans32(blk, 0, (uint32_t)(ps / ZC_SPAN));
+        if (ps >= (uint64_t)W + m) {
+          carry = *(const uint4*)(data + ps - W - m);
+        } else if (ps + 16 > (uint64_t)W + m) {  // the piece straddles the stream start
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (uint32_t i = 0; i < 16; ++i) {
+            const int64_t at = (int64_t)ps - (int64_t)W - (int64_t)m + i;
+            if (at >= 0) w[i >> 2] |= (uint32_t)data[at] << (8 * (i & 3));
+          }
+          carry = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+      head = wtbase < (uint64_t)W + 16;
+      need_valid = wtbase < p_start || wtbase + ZC_FWT > n;
       open = false;
       open_mask = 0;
       ovf = false;
@@ -1258,9 +1294,19 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
 
 #pragma unroll
     for (int p = 0; p < kFPieces; ++p) {
+      const uint64_t pp = ps + (uint64_t)r * ZC_FROUND + 16 * p;  // first position of the piece
       const uint4 vout = funnel16<Q>(p == 0 ? carry : vst[p - 1], vst[p], sbyte);
       const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
-      const uint32_t xout[4] = {vout.x, vout.y, vout.z, vout.w};
+      uint32_t xout[4] = {vout.x, vout.y, vout.z, vout.w};
+      if (head && pp < W) {
+        // out-bytes b[pp - W + i] with pp - W + i < 0 are zero
+        const uint64_t z = (uint64_t)W - pp;  // bytes of the piece to clear
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint64_t lo = 4 * d;
+          xout[d] = z >= lo + 4 ? 0u : (z > lo ? xout[d] & (~0u << (8 * (z - lo))) : xout[d]);
+        }
+      }
       const uint32_t V0 = V;
       uint64_t any = 0, all = ~0ull;
 #pragma unroll
@@ -1273,11 +1319,11 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
           all &= b;
         }
       uint64_t need = (open_mask & ~all) | (~open_mask & any);
-      const uint64_t pp = ps + (uint64_t)r * ZC_FROUND + 16 * p;  // first position of the piece
       if (need_valid) {
-        const uint64_t none = __ballot(pp + 16 <= p_start);
-        const uint64_t some = __ballot(pp < p_start);  // at least one position before p_start
-        need = (need & ~some) | (some & ~none & (any | open_mask));
+        // pieces with positions outside [p_start, n): lanes with hits or an
+        // open run take the exact path (it closes runs at n)
+        const uint64_t some = __ballot(pp < p_start || pp + 16 > n);
+        need = (need & ~some) | (some & (any | open_mask));
       }
       if (__builtin_expect(need != 0, 0)) {
         if ((need >> lane) & 1) {
@@ -1288,7 +1334,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
             for (int q = 0; q < 4; ++q) {
               Vx = Vx * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - ((xout[d] >> (8 * q)) & 0xFFu) * pw32;
               const uint64_t pos = pp + 4 * d + q;
-              const bool h = f_hit<NF>(Vx, K, s_map, pw32) && pos >= p_start;
+              const bool h = f_hit<NF>(Vx, K, s_map, pw32) && pos >= p_start && pos < n;
               const uint32_t rel = (uint32_t)(pos - wtbase);
               if (h && !open) {
                 open = true;
@@ -1610,14 +1656,14 @@ hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, ui
 }
 
 template <int Q>
-static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, const uint8_t* data,
+static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, const uint8_t* data, uint64_t n,
                                         const uint64_t* blk, uint32_t W, uint32_t pw32, uint32_t sbyte,
                                         uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* fmap,
                                         Run* runs, uint64_t runs_cap, uint64_t* wt_off, uint32_t* wt_cnt,
                                         unsigned long long* counters) {
 #define ZC_FS(NF)                                                                                                  \
-  hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(ZC_FTPB), 0, s, data, blk, W, pw32, sbyte, \
-                     p_start, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
+  hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(ZC_FTPB), 0, s, data, n, blk, W, pw32,     \
+                     sbyte, p_start, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
   if (nfk == 1) ZC_FS(1);
   else if (nfk == 4) ZC_FS(4);
   else ZC_FS(0);
@@ -1625,12 +1671,12 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
   return hipGetLastError();
 }
 
-hipError_t launch_fscan_staged(const uint8_t* data, const uint64_t* blk, uint32_t W, uint32_t pw32,
+hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                                uint64_t p_start, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
                                uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
                                uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
-  if (W < 32 || wt0 * ZC_FWT < (uint64_t)W + 16 || nf == 0) return hipErrorInvalidValue;
+  if (W < 32 || n < 64 || (wt0 + nwt - 1) * ZC_FWT >= n || nf == 0) return hipErrorInvalidValue;
   FKeys K;
   const int nfk = nf == 1 ? 1 : nf <= 4 ? 4 : 0;
   for (int i = 0; i < 4; ++i) K.k[i] = (nfk != 0 ? keys32[i < (int)nf ? i : 0] : 0u) - pw32;
@@ -1638,13 +1684,13 @@ hipError_t launch_fscan_staged(const uint8_t* data, const uint64_t* blk, uint32_
   const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * (ZC_FTPB / 64));
   const unsigned grid = (waves + ZC_FTPB / 64 - 1) / (ZC_FTPB / 64);
   switch (m >> 2) {
-    case 0: return launch_fscan_staged_q<0>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+    case 0: return launch_fscan_staged_q<0>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
                                             runs, runs_cap, wt_off, wt_cnt, counters);
-    case 1: return launch_fscan_staged_q<1>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+    case 1: return launch_fscan_staged_q<1>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
                                             runs, runs_cap, wt_off, wt_cnt, counters);
-    case 2: return launch_fscan_staged_q<2>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+    case 2: return launch_fscan_staged_q<2>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
                                             runs, runs_cap, wt_off, wt_cnt, counters);
-    default: return launch_fscan_staged_q<3>(nfk, grid, s, data, blk, W, pw32, m & 3, p_start, wt0, nwt, K,
+    default: return launch_fscan_staged_q<3>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K,
                                              fbits17, runs, runs_cap, wt_off, wt_cnt, counters);
   }
 }
