@@ -370,7 +370,6 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 constexpr int kRounds = ZC_LSPAN / ZC_ROUND;  // rounds per tile (plus one warm-up round)
 constexpr int kDmaRound = 64 * ZC_ROUND / 1024;  // DMA instructions per wave-round
-constexpr int kDmaWarm = 2;                      // ... per warm-up round (64 x 32 B)
 constexpr int kDigests = ZC_LSPAN / ZC_SPAN;     // span digests per lane span
 
 // LDS image of a wave-round: row i (lane i's ZC_ROUND bytes) is stored
@@ -395,26 +394,42 @@ __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, ui
                                      0, 0);
 }
 
-// DMA of the warm-up round of `tile`: the 32 bytes before each of the wave's
-// 64 spans (they prime the gear), row-major 32 B per row, two instructions.
-// Span 0 of the stream has no bytes before it: its lanes read the span itself
-// instead (the gear of span 0 starts from zero and ignores them).
-__device__ __forceinline__ void stage_warmup(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
-                                             uint32_t lane, uint64_t tile, uint32_t slot) {
-  uint8_t* dst = ring + slot * (64 * ZC_ROUND);
-  const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN;
-#pragma unroll
-  for (int j = 0; j < kDmaWarm; ++j) {
-    const uint64_t row = (uint64_t)j * 32 + lane / 2;
-    const uint64_t at = tile0 + row * ZC_LSPAN + (lane & 1) * 16;
-    const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(dst + j * 1024), 16, 0, 0);
-  }
-}
-
 template <int N>
 __device__ __forceinline__ void wait_lgkmcnt() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Loads the hand-counted vmcnt waits order, written as inline asm so the
+// compiler's own wait insertion does not track them: it cannot follow the
+// counts across loop iterations and would put an s_waitcnt vmcnt(0) before
+// every use (draining the prefetched rounds).  LDS reads of a ring slot the
+// DMA fills are the same case (any DS read of the ring array may alias an
+// outstanding LDS-DMA).  ties(v) pins the values after the wait that covers
+// them.
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4u32 lds_read16(const uint8_t* p) {
+  v4u32 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ v4u32 global_read16(const uint8_t* p) {
+  v4u32 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint4 to_uint4(v4u32 v) { return make_uint4(v[0], v[1], v[2], v[3]); }
+template <int N>
+__device__ __forceinline__ void ties(v4u32 (&v)[N]) {
+  static_assert(N == 2 || N == 4 || N == 8, "ties");
+  if constexpr (N == 2) {
+    asm volatile("" : "+v"(v[0]), "+v"(v[1])::"memory");
+  } else if constexpr (N == 4) {
+    asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
+  } else {
+    asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                 "+v"(v[7])::"memory");
+  }
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform n < 40 (the tile end's store count is
@@ -528,11 +543,13 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   return kDigests / 2 + 3;
 }
 
-// The workgroup's rounds form one flat sequence over its tiles (33 per tile:
-// the warm-up round, then 32).  A round is read from its ring slot into
-// registers first; the slot is then refilled with the round two ahead before
-// the round is hashed, so two rounds (16 KiB per wave) are in flight while a
-// wave computes.
+// The workgroup's rounds form one flat sequence over its tiles (32 per
+// tile).  A round is read from its ring slot into registers first; the slot
+// is then refilled with the round two ahead before the round is hashed, so
+// two rounds (16 KiB per wave) are in flight while a wave computes.  The 32
+// bytes before each lane span (they prime the gear) are two per-lane register
+// loads issued together with the DMA of the tile's first round, so tile
+// boundaries cost no extra pipeline round.
 template <int ABL>
 __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
@@ -540,7 +557,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
   __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
   __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
-  constexpr uint32_t kRpt = kRounds + 1;  // rounds per tile, warm-up included
+  constexpr uint32_t kRpt = kRounds;  // rounds per tile
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t grid = gridDim.x;
   uint8_t* myring = ring[wave];
@@ -556,13 +573,18 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     lane_off[j] = row * ZC_LSPAN + ((lane % kPieces) ^ row_swizzle(row)) * 16;
   }
   const uint32_t sw = row_swizzle(lane);  // read-side swizzle of this lane's row
+  v4u32 warm[2];                          // the 32 bytes before the next tile's span
   auto issue = [&](uint32_t Rx) {
-    const uint32_t k = Rx / kRpt, r1 = Rx - k * kRpt;
+    const uint32_t k = Rx / kRpt, r = Rx - k * kRpt;
     const uint64_t tile = tile0 + blockIdx.x + (uint64_t)k * grid;
-    if (r1 == 0)
-      stage_warmup(data, myring, wave, lane, tile, Rx & 1);
-    else
-      stage_round(data, myring, wave, lane_off, tile, (int)r1 - 1, Rx & 1);
+    stage_round(data, myring, wave, lane_off, tile, (int)r, Rx & 1);
+    if (r == 0) {
+      // span 0 of the stream has no bytes before it: it reads itself (unused)
+      const uint64_t at = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
+      const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
+      warm[0] = global_read16(src);
+      warm[1] = global_read16(src + 16);
+    }
   };
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
@@ -577,35 +599,40 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
 #pragma unroll 1
   for (uint32_t R = 0; R < nR; ++R) {
     const uint32_t k = R / kRpt;
-    const int r = (int)(R - k * kRpt) - 1;
-    // round R has landed once only round R + 1 (if issued) is outstanding
+    const int r = (int)(R - k * kRpt);
+    // round R (and, for a tile's first round, its warm-up loads) has landed
+    // once only what was issued after it is outstanding: round R + 1's DMA,
+    // plus the next tile's warm-up loads after round kRounds - 2, plus the
+    // tile end's stores before round 0
     if (R + 1 >= nR) wait_vmcnt<0>();
-    else if (r == kRounds - 1) wait_vmcnt<kDmaWarm>();  // R + 1 is a warm-up round
-    else if (r < 0) wait_vmcnt_dyn(kDmaRound + tail_stores);  // the tile end's stores may stay in flight
+    else if (r == kRounds - 1) wait_vmcnt<kDmaRound + 2>();
+    else if (r == 0) wait_vmcnt_dyn(kDmaRound + tail_stores);
     else wait_vmcnt<kDmaRound>();
     const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND);
-    if (r < 0) {
-      // warm-up round: the 32 bytes before the span prime the gear
-      const uint4 w0 = *(const uint4*)(row + lane * 32), w1 = *(const uint4*)(row + lane * 32 + 16);
-      wait_lgkmcnt<0>();  // the slot is free
-      if (R + 2 < nR) issue(R + 2);
+    if (r == 0) {
+      // a new tile: the warm-up bytes prime the gear
       span0 = (tile0 + blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
       s = ScanLane{0, 0, 0};
       wl.n = 0;
       last = kNoEntry;
+      ties(warm);  // landed: the wait above covers them
       if (span0 >= 64) {
-        const uint32_t xs[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const uint32_t xs[8] = {warm[0][0], warm[0][1], warm[0][2], warm[0][3],
+                                warm[1][0], warm[1][1], warm[1][2], warm[1][3]};
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
           for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
-      continue;
     }
+    v4u32 vr[kPieces];
+#pragma unroll
+    for (int p = 0; p < kPieces; ++p) vr[p] = lds_read16(row + lane * ZC_ROUND + ((p ^ sw) << 4));
+    wait_lgkmcnt<0>();  // the slot is free
+    ties(vr);
     uint4 v[kPieces];
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) v[p] = *(const uint4*)(row + lane * ZC_ROUND + ((p ^ sw) << 4));
-    wait_lgkmcnt<0>();  // the slot is free
+    for (int p = 0; p < kPieces; ++p) v[p] = to_uint4(vr[p]);
     if (R + 2 < nR) issue(R + 2);
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lo_thr, s, wl, last);
