@@ -201,7 +201,7 @@ def main():
                        "candidates": st["candidates"], "epochs": st["epochs"],
                        "meta_ms": round(st["meta_ms"], 4), "probe_ms": round(st["probe_ms"], 4),
                        "fscan_ms": round(st["fscan_ms"], 4), "walk_ms": round(st["walk_ms"], 4),
-                       "finalize_ms": round(st["finalize_ms"], 4)},
+                       "finalize_ms": round(st["finalize_ms"], 4), "fbatch_ms": round(st["fbatch_ms"], 4)},
         }
         if e2e:
             out["end_to_end"] = e2e

@@ -91,6 +91,7 @@ typedef struct {
   double fscan_ms;       /* exact-hash screen */
   double walk_ms;        /* boundary walk + record assembly on the host */
   double finalize_ms;    /* digests of cut pieces, SHA-1 ids */
+  double fbatch_ms;      /* (part of walk_ms) batched key/byte/SHA-1 checks of screen hits */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;

@@ -37,7 +37,7 @@ class ZcStats(ctypes.Structure):
                 ("epochs", ctypes.c_uint64), ("fscan_runs", ctypes.c_uint64),
                 ("meta_ms", ctypes.c_double), ("probe_ms", ctypes.c_double),
                 ("fscan_ms", ctypes.c_double), ("walk_ms", ctypes.c_double),
-                ("finalize_ms", ctypes.c_double)]
+                ("finalize_ms", ctypes.c_double), ("fbatch_ms", ctypes.c_double)]
 
 
 class ZcError(RuntimeError):

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <iterator>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -170,6 +171,7 @@ struct zc_ctx {
   DevBuf<uint32_t> ancless;
   HostBuf<unsigned long long> h_cnt;
   HostBuf<uint64_t> h_key;  // grid-chunk keys of the current epoch
+  HostBuf<uint64_t> h_ra, h_rb, h_rout;  // pinned staging of range-digest batches
 };
 
 namespace {
@@ -315,6 +317,9 @@ class Resolver {
   }
 
   std::unordered_map<uint64_t, std::vector<uint32_t>> fmap_;  // key -> anchorless refs (start order)
+  std::unordered_map<uint64_t, std::vector<uint32_t>>::iterator fmemo_it_;  // last fmap_ lookup
+  uint64_t fmemo_key_ = 0;
+  bool fmemo_valid_ = false;
   std::unordered_map<uint64_t, std::vector<uint32_t>> smap_;  // key -> statics
   std::vector<Run> runs_;
   uint64_t f_min_vis_ = kInf;
@@ -421,6 +426,7 @@ class Resolver {
     acands_.clear();
     runs_.clear();
     fmap_.clear();
+    fmemo_valid_ = false;
     fb_ = FBatch{};
     has_f_ = false;
     f_min_vis_ = kInf;
@@ -591,11 +597,17 @@ class Resolver {
     c_.va.ensure(nr);
     c_.vb.ensure(nr);
     c_.dout.ensure(nr);
-    h2d(c_, c_.va.p, a.data(), nr);
-    h2d(c_, c_.vb.p, b.data(), nr);
+    c_.h_ra.ensure(nr);
+    c_.h_rb.ensure(nr);
+    c_.h_rout.ensure(nr);
+    memcpy(c_.h_ra.p, a.data(), nr * sizeof(uint64_t));
+    memcpy(c_.h_rb.p, b.data(), nr * sizeof(uint64_t));
+    h2d(c_, c_.va.p, c_.h_ra.p, nr);
+    h2d(c_, c_.vb.p, c_.h_rb.p, nr);
     HCK(launch_range_digest(d_, n_, c_.blk.p, c_.va.p, c_.vb.p, (uint32_t)nr, c_.dout.p, c_.stream));
-    d2h(c_, out.data(), c_.dout.p, nr);
+    d2h(c_, c_.h_rout.p, c_.dout.p, nr);
     sync(c_);
+    memcpy(out.data(), c_.h_rout.p, nr * sizeof(uint64_t));
     return out;
   }
 
@@ -685,12 +697,17 @@ class Resolver {
     }
     const uint64_t nruns = cnt[CNT_RUNS];
     c_.stats.fscan_runs += nruns;
+    // zc_fscan's per-tile lists are read only where it ran
+    bool old_ran = !staged;
+    for (uint32_t c : wcnt) old_ran |= c == ZC_FWT_OVERFLOW;
     std::vector<Run> raw(nruns);
-    std::vector<uint64_t> toff(ntiles), woff(wcnt.size());
-    std::vector<uint32_t> tcnt(ntiles);
+    std::vector<uint64_t> toff(old_ran ? ntiles : 0), woff(wcnt.size());
+    std::vector<uint32_t> tcnt(old_ran ? ntiles : 0);
     d2h(c_, raw.data(), c_.runs.p, nruns);
-    d2h(c_, toff.data(), c_.ftile_off.p, ntiles);
-    d2h(c_, tcnt.data(), c_.ftile_cnt.p, ntiles);
+    if (old_ran) {
+      d2h(c_, toff.data(), c_.ftile_off.p, ntiles);
+      d2h(c_, tcnt.data(), c_.ftile_cnt.p, ntiles);
+    }
     d2h(c_, woff.data(), c_.fwt_off.p + wt_lo, woff.size());
     sync(c_);
     auto take = [&](const Run* q, uint64_t k) {
@@ -736,7 +753,13 @@ class Resolver {
 
   // first alive ref with key h visible at p (start order; vis grows with start)
   int64_t first_alive_ref(uint64_t h, uint64_t p) {
-    auto it = fmap_.find(h);
+    // consecutive screen hits mostly share one key (runs of repeated content)
+    if (!fmemo_valid_ || fmemo_key_ != h) {
+      fmemo_it_ = fmap_.find(h);
+      fmemo_key_ = h;
+      fmemo_valid_ = true;
+    }
+    auto it = fmemo_it_;
     if (it == fmap_.end()) return -1;
     for (uint32_t ref : it->second) {
       if (ref_vis(ref) > p) break;
@@ -746,6 +769,7 @@ class Resolver {
   }
 
   void build_fbatch(uint64_t p0) {
+    const auto t0 = Clock::now();
     FBatch b;
     // predicted positions: p0, p0+1..p0+7 (in case p0 fails), then the
     // success chain p0+W, p0+2W, ... all restricted to screen runs
@@ -767,8 +791,17 @@ class Resolver {
       q += W_;
     }
     irun_ = save;
-    std::sort(pos.begin(), pos.end());
-    pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+    // two ascending lists (the neighbours of p0, then the success chain):
+    // merge them, dropping duplicates
+    {
+      size_t k = 0;
+      while (k + 1 < pos.size() && pos[k] < pos[k + 1]) ++k;
+      std::vector<uint64_t> m;
+      m.reserve(pos.size());
+      std::merge(pos.begin(), pos.begin() + k + 1, pos.begin() + k + 1, pos.end(), std::back_inserter(m));
+      m.erase(std::unique(m.begin(), m.end()), m.end());
+      pos.swap(m);
+    }
     const size_t np = pos.size();
     std::vector<uint64_t> a(np), e(np);
     for (size_t i = 0; i < np; ++i) {
@@ -779,8 +812,9 @@ class Resolver {
     b.pos = std::move(pos);
     b.vref.assign(np, -1);
     b.vok.assign(np, 0);
-    b.has_sha.assign(np, 0);
-    b.sha.assign(np * 20, 0);
+    const bool statics = !smap_.empty();
+    b.has_sha.assign(statics ? np : 0, 0);
+    b.sha.assign(statics ? np * 20 : 0, 0);
     std::vector<uint64_t> wa, ra;
     std::vector<size_t> widx;
     std::vector<uint64_t> sa;
@@ -798,7 +832,7 @@ class Resolver {
           widx.push_back(i);
         }
       }
-      if (smap_.count(b.h[i])) {
+      if (statics && smap_.count(b.h[i])) {
         sa.push_back(a[i]);
         sl.push_back(W_);
         sidx.push_back(i);
@@ -812,6 +846,7 @@ class Resolver {
       memcpy(&b.sha[sidx[j] * 20], &sh[j * 20], 20);
     }
     fb_ = std::move(b);
+    c_.stats.fbatch_ms += ms_since(t0);
   }
 
   // Is p an F match?  Returns the matched key via *key.
@@ -821,6 +856,8 @@ class Resolver {
     const size_t i = fb_.cur;
     const uint64_t h = fb_.h[i];
     *key = h;
+    // the batch's witness is still in the index: the common case
+    if (fb_.vref[i] >= 0 && fb_.vok[i] && class_alive_visible((uint32_t)fb_.vref[i], p)) return true;
     // in-stream anchorless chunks: content equality with an alive visible ref
     auto it = fmap_.find(h);
     if (it != fmap_.end()) {

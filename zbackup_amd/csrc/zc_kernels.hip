@@ -381,17 +381,19 @@ __host__ __device__ constexpr uint32_t row_swizzle(uint32_t row) { return (row /
 
 // DMA of round r of `tile` into ring slot `slot`: ZC_ROUND bytes of each of
 // the wave's 64 rows; one instruction fills 1024 / ZC_ROUND rows (1 KiB).
-// The per-lane part of the source address (lane_off[j]) is loop-invariant;
-// the rest is wave-uniform.
+// Through a buffer descriptor at the wave-round's first byte (wave-uniform,
+// built with scalar instructions): the lane's part of every instruction is
+// its loop-invariant 32-bit offset lane_off[j], so a round costs no vector
+// address arithmetic.  (wave must be wave-uniform: readfirstlane'd.)
 __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
                                             const uint32_t (&lane_off)[kDmaRound], uint64_t tile, int r,
                                             uint32_t slot) {
   uint8_t* dst = ring + slot * (64 * ZC_ROUND);
-  const uint64_t tile0 = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)r * ZC_ROUND;
+  const uint64_t at = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)r * ZC_ROUND;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(data + at), (short)0, 64 * ZC_LSPAN, 0x00020000);
 #pragma unroll
   for (int j = 0; j < kDmaRound; ++j)
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + tile0 + lane_off[j]), (lds_void_t*)(dst + j * 1024), 16,
-                                     0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + j * 1024), 16, (int)lane_off[j], 0, 0, 0);
 }
 
 template <int N>
@@ -558,7 +560,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
   __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
   constexpr uint32_t kRpt = kRounds;  // rounds per tile
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t grid = gridDim.x;
   uint8_t* myring = ring[wave];
   WaveList wl{wlist[wave], wdata[wave], 0};
@@ -1214,10 +1216,11 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
     __syncthreads();
   }
   const uint32_t m = (uint32_t)(4 * Q) + sbyte;  // = -W mod 16
-  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave, nw = (uint64_t)gridDim.x * kWaves;
+  const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform (scalar descriptors)
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave_u, nw = (uint64_t)gridDim.x * kWaves;
   const uint32_t ntk = nwt > gw ? (uint32_t)((nwt - 1 - gw) / nw + 1) : 0;
   const uint32_t nR = ntk * kFRounds;
-  uint8_t* myring = ring[wave][0];
+  uint8_t* myring = ring[wave_u][0];
   uint32_t* lrs = s_rs[wave];
   uint32_t* lre = s_re[wave];
   // this lane's share of DMA instruction j (rows 8 KiB apart, source piece
@@ -1230,32 +1233,32 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
   }
   const uint32_t sw = frow_swizzle(lane);
   const uint64_t out_shift = (uint64_t)W + m - 16;  // staged out-row = in-row - out_shift
-  // the stream's first and last wave-tiles: source pieces before the stream
-  // or past its end are read from a valid piece instead (their bytes are
-  // never used: out-bytes before the stream count as zero, positions past
-  // the end are not screened)
-  const uint64_t last16 = (n - 16) & ~15ull;
+  // DMA through buffer descriptors rebuilt per round (scalar work only): the
+  // lane's part of each instruction is its loop-invariant 32-bit offset, and
+  // the descriptor's range check makes pieces past the stream end read as
+  // zero.  Out-rows before the stream start (the first wave-tiles) get a
+  // wrapped offset, out of range as well; their bytes are cleared anyway.
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kFRounds, r = Rx - k * kFRounds;
-    const uint64_t wtile = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT;
-    const uint64_t wtb = wtile + (uint64_t)r * ZC_FROUND;
-    const bool edge = wtile < out_shift + ZC_FWT || wtile + ZC_FWT > n;
+    const uint64_t at = (wt0 + gw + (uint64_t)k * nw) * ZC_FWT + (uint64_t)r * ZC_FROUND;
     uint8_t* dst = myring + (Rx & 1) * (2 * kSlot);
+    const uint64_t in_left = n - at;  // > 0: every issued round starts inside the stream
+    const auto rin = __builtin_amdgcn_make_buffer_rsrc((void*)(data + at), (short)0,
+                                                       (int)(in_left < 0x7FFFFFF0ull ? in_left : 0x7FFFFFF0ull),
+                                                       0x00020000);
+    const uint64_t ob = at >= out_shift ? at - out_shift : 0;
+    const uint32_t oadj = at >= out_shift ? 0u : (uint32_t)(at - out_shift);  // wraps: out of range
+    const uint64_t out_left = n - ob;
+    const auto rout = __builtin_amdgcn_make_buffer_rsrc((void*)(data + ob), (short)0,
+                                                        (int)(out_left < 0x7FFFFFF0ull ? out_left : 0x7FFFFFF0ull),
+                                                        0x00020000);
 #pragma unroll
-    for (int j = 0; j < kFDmaHalf; ++j) {
-      uint64_t a = wtb + lane_off[j];
-      if (edge && a > last16) a = last16;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + a), (lds_void_t*)(dst + j * 1024), 16, 0, 0);
-    }
+    for (int j = 0; j < kFDmaHalf; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void_t*)(dst + j * 1024), 16, (int)lane_off[j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < kFDmaHalf; ++j) {
-      uint64_t a = wtb + lane_off[j] - out_shift;
-      if (edge) {
-        const uint64_t in = wtb + lane_off[j];
-        a = in < out_shift ? 0 : (a > last16 ? last16 : a);
-      }
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + a), (lds_void_t*)(dst + kSlot + j * 1024), 16, 0, 0);
-    }
+    for (int j = 0; j < kFDmaHalf; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rout, (lds_void_t*)(dst + kSlot + j * 1024), 16,
+                                               (int)(lane_off[j] + oadj), 0, 0, 0);
   };
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
