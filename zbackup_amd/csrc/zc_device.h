@@ -155,15 +155,19 @@ hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64
                           unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s);
-hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,
-                               const uint32_t* cg, const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs,
+// table of class leaders' first anchors (2^tbits slots of 16 bytes: 2 << tbits
+// words of tab) and its key filter gfilt (probe_filter_words() words); both
+// cleared and filled here
+hipError_t launch_table_insert(uint64_t* tab, uint32_t tbits, const uint32_t* cg, const uint64_t* cfp,
+                               const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs, uint32_t* gfilt,
                                hipStream_t s);
+uint32_t probe_filter_words();
 
-// one wave per wave-tile: every anchor of the stream probes the table
-hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tkeys,
-                        const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp,
-                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t n, uint32_t W, Cand* cand,
-                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
+// every anchor of the stream probes the filter, then the table
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tab, uint32_t tbits,
+                        const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis, const uint8_t* dead,
+                        uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
+                        unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,

@@ -157,9 +157,10 @@ struct zc_ctx {
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
   DevBuf<uint32_t> c_anc, c_g;
   DevBuf<uint8_t> c_dead;
-  DevBuf<uint64_t> tkeys, ckeys;
+  DevBuf<uint64_t> ckeys;
   DevBuf<uint32_t> cvals, c_cls;
-  DevBuf<uint32_t> tvals;
+  DevBuf<uint64_t> tab;     // anchor table: 16-byte slots {gear | ref << 32, fingerprint}
+  DevBuf<uint32_t> gfilt;   // its key filter
   DevBuf<Cand> cand;
   DevBuf<uint64_t> va, vb, dout;
   DevBuf<uint32_t> vlen;
@@ -465,14 +466,13 @@ class Resolver {
       HCK(launch_classes(d_, c_.c_key.p, c_.c_start.p, nref_, W_, c_.ckeys.p, c_.cvals.p, tbits, c_.c_cls.p,
                          c_.counters.p, c_.stream));
       if (npool_) {
-        c_.tkeys.ensure(1u << tbits);
-        c_.tvals.ensure(1u << tbits);
+        c_.tab.ensure(2u << tbits);
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
-        HCK(launch_table_clear(c_.tkeys.p, 1u << tbits, c_.stream));
-        HCK(launch_table_insert(c_.tkeys.p, c_.tvals.p, tbits, c_.c_g.p, c_.c_anc.p, c_.c_cls.p, nref_,
+        c_.gfilt.ensure(probe_filter_words());
+        HCK(launch_table_insert(c_.tab.p, tbits, c_.c_g.p, c_.c_fp.p, c_.c_anc.p, c_.c_cls.p, nref_, c_.gfilt.p,
                                 c_.stream));
-        HCK(launch_probe(d_, av_, nwt_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
-                         c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av_, nwt_, c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p, c_.c_dead.p, r_e_, n_,
+                         W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       }
       HCK(launch_anchorless(c_.c_anc.p, c_.c_cls.p, nref_, c_.ancless.p, nref_, c_.counters.p, c_.stream));
       d2h(c_, c_.h_key.p, c_.c_key.p + nconf_, nsref);
@@ -484,8 +484,8 @@ class Resolver {
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-        HCK(launch_probe(d_, av_, nwt_, c_.tkeys.p, c_.tvals.p, tbits, c_.c_anc.p, c_.c_fp.p, c_.c_vis.p,
-                         c_.c_dead.p, r_e_, n_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av_, nwt_, c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p, c_.c_dead.p, r_e_, n_,
+                         W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
         ncand = c_.h_cnt[CNT_CAND];

@@ -86,7 +86,18 @@ __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __r
   for (uint64_t i = a; i < a_up; ++i) acc = acc * 257u + data[i];
   uint64_t b_dn = b / ZC_SPAN * ZC_SPAN;
   const uint64_t m = span_mul();
-  for (uint64_t k = a_up / ZC_SPAN; k < b_dn / ZC_SPAN; ++k) acc = acc * m + blk[k];
+  uint64_t k = a_up / ZC_SPAN;
+  const uint64_t k1 = b_dn / ZC_SPAN;
+  // span digests eight loads at a time (the fold is a dependent chain; the
+  // loads need not be)
+  for (; k + 8 <= k1; k += 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = blk[k + i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = acc * m + v[i];
+  }
+  for (; k < k1; ++k) acc = acc * m + blk[k];
   for (uint64_t i = b_dn; i < b; ++i) acc = acc * 257u + data[i];
   return acc;
 }
@@ -154,22 +165,16 @@ __device__ __forceinline__ void digest_step(uint32_t b, ScanLane& s) {
   s.hhi = (uint32_t)(h >> 32);
 }
 
-// 64-bit fingerprint of the 64 bytes ending at anchor position q (q >= 63).
+// 64-bit fingerprint of anchor position q (q >= 63).
 // Computed lazily from HBM -- only for chunk first-anchors and for stream
 // anchors whose gear value hits the table -- so the scan keeps no per-byte
 // fingerprint state.  Any fixed function of those bytes works: both sides
 // (chunks and stream windows) use this one.
 __device__ __forceinline__ uint32_t load4_any(const uint8_t* base, uint64_t addr);
 __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
-  uint64_t h = 0x243F6A8885A308D3ull;
-  const uint64_t a = q - (ZC_ANCHOR_MIN_OFF);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    h ^= load4_any(data, a + 4 * i);
-    h *= kGolden;
-    h ^= h >> 29;
-  }
-  return h;
+  // the 8 bytes ending at q (the gear value adds the 32 before; an anchor's
+  // gear has only ~20 free bits, these 64 make a false match rare)
+  return ((uint64_t)load4_any(data, q - 3) << 32) | load4_any(data, q - 7);
 }
 
 // Ablation bits (tools/ubench/scan_ablate.hip only; the product uses 0):
@@ -763,8 +768,9 @@ __global__ void zc_anchorless_kernel(const uint32_t* __restrict__ anc_off, const
 }
 
 // ---------------------------------------------------------------------------
-// anchor table: open addressing on the anchor's gear value, duplicates kept;
-// the 64-bit fingerprint is compared on a hit
+// anchor table: open addressing on the anchor's gear value, duplicates kept.
+// A slot is 16 bytes, {gear | ref << 32, fingerprint}: one load gives the
+// key, the ref and the fingerprint to compare (empty: all ones).
 constexpr uint64_t kEmpty = ~0ull;
 
 __global__ void zc_table_clear_kernel(uint64_t* tkeys, uint32_t tsize) {
@@ -776,20 +782,26 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
   return (uint32_t)(((uint64_t)g * kGolden) >> (64 - tbits));
 }
 
-__global__ void zc_table_insert_kernel(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits,
-                                       const uint32_t* __restrict__ cg,
-                                       const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
-                                       uint32_t nrefs) {
+// the probe's first level: bit (g mod 2^kGFiltBits) of every table key (the
+// low bits: an anchor's gear always has its top bits set)
+constexpr int kGFiltBits = 20;                               // 2^20 bits = 128 KiB
+constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
+
+__global__ void zc_table_insert_kernel(uint64_t* tab, uint32_t tbits, const uint32_t* __restrict__ cg,
+                                       const uint64_t* __restrict__ cfp, const uint32_t* __restrict__ anc_off,
+                                       const uint32_t* __restrict__ cls, uint32_t nrefs, uint32_t* __restrict__ gfilt) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nrefs || anc_off[i] == ZC_NO_ANCHOR || cls[i] != i) return;
-  const uint64_t k = cg[i];
+  const uint32_t fb = cg[i] & ((1u << kGFiltBits) - 1);
+  atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
+  const uint64_t word = ((uint64_t)i << 32) | cg[i];
   const uint32_t mask = (1u << tbits) - 1;
   uint32_t h = table_slot(cg[i], tbits);
   for (;;) {
-    unsigned long long prev = atomicCAS((unsigned long long*)&tkeys[h], (unsigned long long)kEmpty,
-                                        (unsigned long long)k);
+    unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
+                                        (unsigned long long)word);
     if (prev == kEmpty) {
-      tvals[h] = i;
+      tab[2 * (uint64_t)h + 1] = cfp[i];
       return;
     }
     h = (h + 1) & mask;
@@ -797,55 +809,107 @@ __global__ void zc_table_insert_kernel(uint64_t* tkeys, uint32_t* tvals, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// zc_probe: one wave per wave-tile, a lane per anchor; every anchor probes the
-// table (key = gear value, confirmed by the 64-byte fingerprint)
-__global__ void __launch_bounds__(256) zc_probe_kernel(const uint8_t* __restrict__ data, AnchorView av,
-                                                       uint64_t nwt, const uint64_t* __restrict__ tkeys,
-                                                       const uint32_t* __restrict__ tvals, uint32_t tbits,
-                                                       const uint32_t* __restrict__ anc_off,
-                                                       const uint64_t* __restrict__ cfp,
-                                                       const uint64_t* __restrict__ vis,
-                                                       const uint8_t* __restrict__ dead, uint64_t r, uint64_t n,
-                                                       uint32_t W, Cand* __restrict__ cand, uint64_t cand_cap,
-                                                       unsigned long long* __restrict__ counters) {
-  const uint64_t wt = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  if (wt >= nwt) return;
-  const TileAnchors ta = tile_anchors(av, wt);
+// zc_probe: every anchor of the stream probes the table (key = gear value,
+// confirmed by the 64-byte fingerprint).  A wave takes kProbeWT consecutive
+// wave-tiles and a lane their slots lane, lane + 64, ... (kProbeSlots per
+// wave-tile; slots past that -- dense small-W streams, side-pool wave-tiles --
+// in a second loop).
+// The loads are issued level by level -- every slot's gear value, then every
+// filter word -- so a lane has all of them in flight at once; an anchor
+// tests the table's 2^20-bit key filter (L2 resident, ~1 in 8 pass at
+// W = 64 KiB) and only then walks the table.
+constexpr int kProbeWT = 2;     // wave-tiles per wave
+constexpr int kProbeSlots = 4;  // slots per lane per wave-tile (covers wcap <= 256)
+
+__device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
+                                             const uint64_t* __restrict__ tab, uint32_t tbits,
+                                             const uint32_t* __restrict__ anc_off, const uint64_t* __restrict__ vis,
+                                             const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W,
+                                             Cand* __restrict__ cand, uint64_t cand_cap,
+                                             unsigned long long* __restrict__ counters) {
+  if (pos < r + ZC_ANCHOR_MIN_OFF) return;
   const uint32_t mask = (1u << tbits) - 1;
-  for (uint32_t e = lane; e < ta.cnt; e += 64) {
-    const uint64_t pos = (wt << ZC_WT_SHIFT) + ta.rel[e];
-    if (pos < r + ZC_ANCHOR_MIN_OFF) continue;
-    const uint32_t gk = ta.g[e];
-    const uint64_t k = gk;
-    uint32_t h = table_slot(gk, tbits);
-    bool have_fp = false;
-    uint64_t fp = 0;
-    for (;;) {
-      const uint64_t tk = tkeys[h];
-      if (tk == kEmpty) break;
-      if (tk == k) {
-        const uint32_t ref = tvals[h];
+  uint32_t h = table_slot(gk, tbits);
+  bool have_fp = false;
+  uint64_t fp = 0;
+  for (;;) {
+    const uint4 slot = *(const uint4*)(tab + 2 * (uint64_t)h);
+    if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
+    if (slot.x == gk) {
+      if (!have_fp) {
+        fp = anchor_fp(data, pos);
+        have_fp = true;
+      }
+      if (fp == (((uint64_t)slot.w << 32) | slot.z)) {
+        const uint32_t ref = slot.y;
         const uint64_t o = anc_off[ref];
         if (pos >= r + o) {
           const uint64_t ws = pos - o, p = ws + W - 1;
           if (p < n && p >= vis[ref] && !dead[ref]) {
-            if (!have_fp) {
-              fp = anchor_fp(data, pos);
-              have_fp = true;
-            }
-            if (fp == cfp[ref]) {
-              const unsigned long long slot = atomicAdd(&counters[CNT_CAND], 1ull);
-              if (slot < cand_cap) {
-                cand[slot].p = p;
-                cand[slot].ref = ref;
-                cand[slot].pad = 0;
-              }
+            const unsigned long long c = atomicAdd(&counters[CNT_CAND], 1ull);
+            if (c < cand_cap) {
+              cand[c].p = p;
+              cand[c].ref = ref;
+              cand[c].pad = 0;
             }
           }
         }
       }
-      h = (h + 1) & mask;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__global__ void __launch_bounds__(256) zc_probe_kernel(
+    const uint8_t* __restrict__ data, AnchorView av, uint64_t nwt, const uint64_t* __restrict__ tab, uint32_t tbits,
+    const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off, const uint64_t* __restrict__ vis,
+    const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W, Cand* __restrict__ cand,
+    uint64_t cand_cap, unsigned long long* __restrict__ counters) {
+  const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  constexpr int kS = kProbeWT * kProbeSlots;
+  uint64_t wts[kProbeWT];
+  TileAnchors ta[kProbeWT];
+#pragma unroll
+  for (int t = 0; t < kProbeWT; ++t) {
+    wts[t] = gwave * kProbeWT + t;
+    ta[t] = wts[t] < nwt ? tile_anchors(av, wts[t]) : TileAnchors{av.rel, av.g, 0u};
+  }
+  // level 1: the gear value of every slot
+  uint32_t g[kS];
+  bool live[kS];
+#pragma unroll
+  for (int q = 0; q < kS; ++q) {
+    const int t = q / kProbeSlots;
+    const uint32_t e = lane + 64u * (q % kProbeSlots);
+    live[q] = e < ta[t].cnt;
+    g[q] = live[q] ? ta[t].g[e] : 0u;
+  }
+  // level 2: the filter word of every live slot
+  uint32_t f[kS];
+#pragma unroll
+  for (int q = 0; q < kS; ++q) {
+    const uint32_t fb = g[q] & ((1u << kGFiltBits) - 1);
+    f[q] = live[q] ? (gfilt[fb >> 5] >> (fb & 31)) & 1u : 0u;
+  }
+  // level 3: the rare anchors that pass walk the table
+#pragma unroll
+  for (int q = 0; q < kS; ++q) {
+    if (!f[q]) continue;
+    const int t = q / kProbeSlots;
+    const uint32_t e = lane + 64u * (q % kProbeSlots);
+    probe_anchor(data, (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e], g[q], tab, tbits, anc_off, vis, dead, r, n, W, cand,
+                 cand_cap, counters);
+  }
+  // wave-tiles with more anchors than the slots above
+#pragma unroll
+  for (int t = 0; t < kProbeWT; ++t) {
+    for (uint32_t e = lane + 64u * kProbeSlots; e < ta[t].cnt; e += 64) {
+      const uint32_t gk = ta[t].g[e];
+      const uint32_t fb = gk & ((1u << kGFiltBits) - 1);
+      if ((gfilt[fb >> 5] >> (fb & 31)) & 1u)
+        probe_anchor(data, (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e], gk, tab, tbits, anc_off, vis, dead, r, n, W,
+                     cand, cand_cap, counters);
     }
   }
 }
@@ -1625,13 +1689,19 @@ hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_table_insert(uint64_t* tkeys, uint32_t* tvals, uint32_t tbits, const uint32_t* cg,
-                               const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs, hipStream_t s) {
-  if (!nrefs) return hipSuccess;
-  hipLaunchKernelGGL(zc_table_insert_kernel, dim3(blocks_for(nrefs, 256)), dim3(256), 0, s, tkeys,
-                     tvals, tbits, cg, anc_off, cls, nrefs);
+hipError_t launch_table_insert(uint64_t* tab, uint32_t tbits, const uint32_t* cg, const uint64_t* cfp,
+                               const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs, uint32_t* gfilt,
+                               hipStream_t s) {
+  hipError_t e = hipMemsetAsync(tab, 0xFF, (size_t)16 << tbits, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(gfilt, 0, kGFiltWords * sizeof(uint32_t), s);
+  if (e != hipSuccess || !nrefs) return e;
+  hipLaunchKernelGGL(zc_table_insert_kernel, dim3(blocks_for(nrefs, 256)), dim3(256), 0, s, tab, tbits, cg, cfp,
+                     anc_off, cls, nrefs, gfilt);
   return hipGetLastError();
 }
+
+uint32_t probe_filter_words() { return kGFiltWords; }
 
 hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64_t* start, uint32_t nref, uint32_t W,
                           uint64_t* ckeys, uint32_t* cvals, uint32_t cbits, uint32_t* cls,
@@ -1648,13 +1718,14 @@ hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64
   return hipGetLastError();
 }
 
-hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tkeys,
-                        const uint32_t* tvals, uint32_t tbits, const uint32_t* anc_off, const uint64_t* cfp,
-                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t n, uint32_t W, Cand* cand,
-                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tab, uint32_t tbits,
+                        const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis, const uint8_t* dead,
+                        uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
+                        unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
-  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(nwt * 64, 256)), dim3(256), 0, s, data, av, nwt, tkeys,
-                     tvals, tbits, anc_off, cfp, vis, dead, r, n, W, cand, cand_cap, counters);
+  const uint64_t waves = (nwt + kProbeWT - 1) / kProbeWT;
+  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(waves * 64, 256)), dim3(256), 0, s, data, av, nwt, tab, tbits,
+                     gfilt, anc_off, vis, dead, r, n, W, cand, cand_cap, counters);
   return hipGetLastError();
 }
 
