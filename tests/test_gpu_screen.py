@@ -70,13 +70,15 @@ def test_many_runs_per_span_overflow(torch_cuda):
     # zero runs slightly longer than W between short random bursts: every
     # 8 KiB lane span holds many separate hit runs, so the staged kernel's
     # wave-tiles overflow their run slots and are redone by zc_fscan
+    # (every zero window after a burst is a grid-shifting match: ~4500 epochs,
+    # each bounded by its horizon)
     W = 200
     parts = [f"Z:{W + 50}"]
-    for i in range(9000):
+    for i in range(4500):
         parts.append(f"R{i + 7}:{7 + i % 13}")
         parts.append(f"Z:{W + 40 + i % 37}")
     data = oracle.gen(",".join(parts))
-    assert data.size > (2 << 20)
+    assert data.size > (1 << 20)
     _check(torch_cuda, data, W)
 
 

@@ -163,10 +163,11 @@ hipError_t launch_table_insert(uint64_t* tab, uint32_t tbits, const uint32_t* cg
                                hipStream_t s);
 uint32_t probe_filter_words();
 
-// every anchor of the stream probes the filter, then the table
-hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tab, uint32_t tbits,
-                        const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis, const uint8_t* dead,
-                        uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
+// every anchor of wave-tiles [wt0, wt0 + nwt) probes the filter, then the
+// table; candidate windows start at >= r (the reset point) and end before p_end
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
+                        uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis,
+                        const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand, uint64_t cand_cap,
                         unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
@@ -186,13 +187,13 @@ hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, ui
                         uint64_t* tile_off, uint32_t* tile_cnt, unsigned long long* counters, hipStream_t s);
 
 // exact screen, staged: screen wave-tiles [wt0, wt0 + nwt) of ZC_FWT bytes,
-// each starting inside the stream (W >= 32, n >= 64), positions p in
-// [p_start, n); keys32 (host memory): nf <= 4 compared directly, else the
+// each starting before p_end <= n (W >= 32, n >= 64), positions p in
+// [p_start, p_end); keys32 (host memory): nf <= 4 compared directly, else the
 // 2^17-bit map fbits17 (device, bit (h >> 15)); wt_cnt[wt] =
 // ZC_FWT_OVERFLOW marks a wave-tile whose runs did not fit (to be redone by
 // launch_fscan)
 hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
-                               uint64_t p_start, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
+                               uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
                                uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
                                uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s);
 

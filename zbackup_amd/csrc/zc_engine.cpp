@@ -22,6 +22,12 @@
 //     otherwise a new epoch recomputes the grid chunks from r.
 //   * Finish (backup_creator.cc:147-172): the pending bytes plus the ring,
 //     as one piece or as a W-byte chunk and the remainder.
+//   * Horizons.  The first epoch covers the whole stream.  An epoch started by
+//     a grid-shifting match covers probes up to a horizon kHorizon0 bytes
+//     ahead; if it reaches the horizon without one, the grid chunks saved by
+//     then become confirmed refs and the next epoch resumes at the horizon
+//     (same grid, the horizon doubled).  Device work per epoch is bounded by
+//     the bytes it covers, so a stream with many grid shifts stays linear.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -123,6 +129,7 @@ constexpr uint64_t kInf = ~0ull;
 constexpr size_t kFeedChunk = 8u << 20;
 constexpr size_t kFBatchMax = 1u << 20;
 constexpr uint64_t kHostSegment = 64ull << 20;  // zc_chunk_host copy/scan pipeline granularity
+constexpr uint64_t kHorizon0 = 256ull << 10;    // first horizon of an epoch after a grid shift (>= 64 W)
 
 }  // namespace
 
@@ -240,6 +247,8 @@ class Resolver {
     for (size_t i = 0; i < c_.statics.size(); ++i) smap_[c_.statics[i].key].push_back((uint32_t)i);
     r_ = 0;
     s_ = 0;
+    x_resume_ = 0;
+    hspan_ = 0;
     while (epoch()) {
     }
     finalize();
@@ -264,8 +273,13 @@ class Resolver {
 
   PoolOut pool_out() { return PoolOut{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, wcap_}; }
 
-  // resolver state
+  // resolver state: reset point r_, bytes saved up to s_, grid origin r_e_ of
+  // the epoch (on r_'s grid: its first chunk not yet saved), its probes
+  // [x_resume_ or r_ + W - 1, h_end_), and the next horizon length hspan_
+  // (0 = to the end of the stream)
   uint64_t r_ = 0, s_ = 0, r_e_ = 0;
+  uint64_t x_resume_ = 0, h_end_ = 0, hspan_ = 0;
+  uint64_t x0() const { return std::max<uint64_t>(r_ + W_ - 1, x_resume_); }
 
   // refs = indexable W-byte chunks that can be matched: [0, nconf_) saved in
   // earlier epochs (visible to every later probe), [nconf_, nref_) this
@@ -416,10 +430,17 @@ class Resolver {
   // back with one synchronisation.
   bool epoch() {
     c_.stats.epochs++;
-    r_e_ = r_;
-    s_ = r_;
+    r_e_ = s_;
     ks_ = 0;
+    const uint64_t xs = x0();
+    h_end_ = hspan_ ? std::min<uint64_t>(n_, xs + hspan_) : n_;
+    // grid chunks cut in the rotate phase (the last W bytes are the ring at
+    // finish), and before the horizon only those cut by a probe below it
     nspec_ = (n_ >= r_e_ + 2ull * W_) ? (uint32_t)((n_ - r_e_ - 2ull * W_) / W_ + 1) : 0;
+    if (h_end_ < n_) {
+      const uint64_t kh = h_end_ - r_e_ >= 2ull * W_ ? (h_end_ - r_e_) / W_ - 1 : 0;  // cut at r_e + (k+2)W - 1 < h_end
+      nspec_ = (uint32_t)std::min<uint64_t>(nspec_, kh);
+    }
     const uint32_t nsref = indexable_ ? nspec_ : 0;
     nref_ = nconf_ + nsref;
     dead_.assign(nref_, 0);
@@ -471,8 +492,8 @@ class Resolver {
         c_.gfilt.ensure(probe_filter_words());
         HCK(launch_table_insert(c_.tab.p, tbits, c_.c_g.p, c_.c_fp.p, c_.c_anc.p, c_.c_cls.p, nref_, c_.gfilt.p,
                                 c_.stream));
-        HCK(launch_probe(d_, av_, nwt_, c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p, c_.c_dead.p, r_e_, n_,
-                         W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p,
+                         c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       }
       HCK(launch_anchorless(c_.c_anc.p, c_.c_cls.p, nref_, c_.ancless.p, nref_, c_.counters.p, c_.stream));
       d2h(c_, c_.h_key.p, c_.c_key.p + nconf_, nsref);
@@ -484,8 +505,8 @@ class Resolver {
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-        HCK(launch_probe(d_, av_, nwt_, c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p, c_.c_dead.p, r_e_, n_,
-                         W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p,
+                         c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
         ncand = c_.h_cnt[CNT_CAND];
@@ -520,6 +541,13 @@ class Resolver {
     c_.stats.walk_ms += ms_since(tw);
     return again;
   }
+
+  // wave-tiles holding the anchors of windows ending in [x0, h_end)
+  uint64_t pwt0() const {
+    const uint64_t xs = x0();
+    return std::min<uint64_t>(nwt_, (xs >= W_ ? xs - W_ + 1 : 0) >> ZC_WT_SHIFT);
+  }
+  uint64_t pwt1() const { return std::max(pwt0(), std::min<uint64_t>(nwt_, ((h_end_ - 1) >> ZC_WT_SHIFT) + 1)); }
 
   // byte-exact verification of every probe candidate window against its chunk
   void verify_candidates(uint64_t nc) {
@@ -642,17 +670,17 @@ class Resolver {
       for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
       h2d(c_, c_.fbits.p, bits.data(), bits.size());
     }
-    const uint64_t p_start = r_e_ + W_ - 1;
-    if (p_start >= n_) return;
+    const uint64_t p_start = x0(), p_end = h_end_;
+    if (p_start >= p_end) return;
     const uint32_t pw32 = (uint32_t)pow257(W_);
-    const uint64_t ntiles = (n_ + ZC_TILE - 1) / ZC_TILE;
+    const uint64_t ntiles = (p_end + ZC_TILE - 1) / ZC_TILE;  // zc_fscan tiles up to the horizon
     // the staged kernel screens wave-tiles [wt_lo, wt_hi) (the whole range
     // from p_start to the end); zc_fscan redoes wave-tiles whose runs
     // overflowed, or everything when the staged kernel does not apply
     const uint64_t t_first = p_start / ZC_TILE;
     const bool staged = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN);
     const uint64_t wt_lo = staged ? p_start / ZC_FWT : 0;
-    const uint64_t wt_hi = staged ? (n_ + ZC_FWT - 1) / ZC_FWT : 0;
+    const uint64_t wt_hi = staged ? (p_end + ZC_FWT - 1) / ZC_FWT : 0;
     constexpr uint64_t kTpw = ZC_FWT / ZC_TILE;  // zc_fscan tiles per screen wave-tile
     c_.ftile_off.ensure(ntiles);
     c_.ftile_cnt.ensure(ntiles);
@@ -670,7 +698,7 @@ class Resolver {
       t0 = std::max(t0, t_first);
       t1 = std::min(t1, ntiles);
       if (t1 > t0)
-        HCK(launch_fscan(d_, n_, c_.blk.p, W_, pw32, p_start, n_, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
+        HCK(launch_fscan(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
                          c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
     };
     std::vector<uint32_t> wcnt(wt_hi - wt_lo);
@@ -678,7 +706,7 @@ class Resolver {
       c_.runs.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
       if (staged) {
-        HCK(launch_fscan_staged(d_, n_, c_.blk.p, W_, pw32, p_start, wt_lo, wt_hi - wt_lo, keys32.data(), nf,
+        HCK(launch_fscan_staged(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(), nf,
                                 c_.fbits17.p, c_.runs.p, c_.runs.cap, c_.fwt_off.p, c_.fwt_cnt.p, c_.counters.p,
                                 c_.stream));
         d2h(c_, wcnt.data(), c_.fwt_cnt.p + wt_lo, wcnt.size());
@@ -956,12 +984,23 @@ class Resolver {
     s_ = n_;
   }
 
+  // the horizon reached without a grid-shifting match: the chunks cut by
+  // then become confirmed refs; the next epoch resumes at the horizon
+  bool horizon_stop() {
+    save_grid_until(h_end_ - 1);
+    keep_saved(h_end_ - 1);
+    x_resume_ = h_end_;
+    hspan_ *= 2;
+    return true;
+  }
+
   bool walk() {
-    uint64_t x = r_ + W_ - 1;
+    uint64_t x = x0();
     size_t ia = 0;
     irun_ = 0;
     for (;;) {
-      if (x >= n_) {
+      if (x >= h_end_) {
+        if (h_end_ < n_) return horizon_stop();
         finish();
         return false;
       }
@@ -977,8 +1016,9 @@ class Resolver {
         ++ia;
       }
       uint64_t fkey = 0;
-      uint64_t pf = next_f(x, pa == kInf ? kInf : pa + 1, &fkey);
+      uint64_t pf = next_f(x, pa == kInf ? h_end_ : pa + 1, &fkey);
       if (pa == kInf && pf == kInf) {
+        if (h_end_ < n_) return horizon_stop();
         finish();
         return false;
       }
@@ -1006,7 +1046,10 @@ class Resolver {
         continue;
       }
       // grid shift: keep the saved chunks of this epoch, start a new one
+      // (its horizon kHorizon0 ahead)
       keep_saved(m);
+      x_resume_ = 0;
+      hspan_ = std::max<uint64_t>(kHorizon0, 64ull * W_);
       return true;
     }
   }

@@ -861,10 +861,10 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
 }
 
 __global__ void __launch_bounds__(256) zc_probe_kernel(
-    const uint8_t* __restrict__ data, AnchorView av, uint64_t nwt, const uint64_t* __restrict__ tab, uint32_t tbits,
-    const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off, const uint64_t* __restrict__ vis,
-    const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W, Cand* __restrict__ cand,
-    uint64_t cand_cap, unsigned long long* __restrict__ counters) {
+    const uint8_t* __restrict__ data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* __restrict__ tab,
+    uint32_t tbits, const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off,
+    const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W,
+    Cand* __restrict__ cand, uint64_t cand_cap, unsigned long long* __restrict__ counters) {
   const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   constexpr int kS = kProbeWT * kProbeSlots;
@@ -872,8 +872,8 @@ __global__ void __launch_bounds__(256) zc_probe_kernel(
   TileAnchors ta[kProbeWT];
 #pragma unroll
   for (int t = 0; t < kProbeWT; ++t) {
-    wts[t] = gwave * kProbeWT + t;
-    ta[t] = wts[t] < nwt ? tile_anchors(av, wts[t]) : TileAnchors{av.rel, av.g, 0u};
+    wts[t] = wt0 + gwave * kProbeWT + t;
+    ta[t] = wts[t] < wt0 + nwt ? tile_anchors(av, wts[t]) : TileAnchors{av.rel, av.g, 0u};
   }
   // level 1: the gear value of every slot
   uint32_t g[kS];
@@ -1266,7 +1266,8 @@ __device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, uint32_t s) {
 template <int Q, int NF>
 __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
     const uint8_t* __restrict__ data, uint64_t n, const uint64_t* __restrict__ blk, uint32_t W, uint32_t pw32,
-    uint32_t sbyte, uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* __restrict__ fmap,
+    uint32_t sbyte, uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, FKeys K,
+    const uint32_t* __restrict__ fmap,
     Run* __restrict__ runs, uint64_t runs_cap, uint64_t* __restrict__ wt_off, uint32_t* __restrict__ wt_cnt,
     unsigned long long* __restrict__ counters) {
   constexpr int kWaves = ZC_FTPB / 64;
@@ -1366,7 +1367,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
         }
       }
       head = wtbase < (uint64_t)W + 16;
-      need_valid = wtbase < p_start || wtbase + ZC_FWT > n;
+      need_valid = wtbase < p_start || wtbase + ZC_FWT > p_end;
       open = false;
       open_mask = 0;
       ovf = false;
@@ -1414,9 +1415,9 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
         }
       uint64_t need = (open_mask & ~all) | (~open_mask & any);
       if (need_valid) {
-        // pieces with positions outside [p_start, n): lanes with hits or an
-        // open run take the exact path (it closes runs at n)
-        const uint64_t some = __ballot(pp < p_start || pp + 16 > n);
+        // pieces with positions outside [p_start, p_end): lanes with hits or
+        // an open run take the exact path (it closes runs at p_end)
+        const uint64_t some = __ballot(pp < p_start || pp + 16 > p_end);
         need = (need & ~some) | (some & (any | open_mask));
       }
       if (__builtin_expect(need != 0, 0)) {
@@ -1428,7 +1429,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
             for (int q = 0; q < 4; ++q) {
               Vx = Vx * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - ((xout[d] >> (8 * q)) & 0xFFu) * pw32;
               const uint64_t pos = pp + 4 * d + q;
-              const bool h = f_hit<NF>(Vx, K, s_map, pw32) && pos >= p_start && pos < n;
+              const bool h = f_hit<NF>(Vx, K, s_map, pw32) && pos >= p_start && pos < p_end;
               const uint32_t rel = (uint32_t)(pos - wtbase);
               if (h && !open) {
                 open = true;
@@ -1718,14 +1719,14 @@ hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64
   return hipGetLastError();
 }
 
-hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t nwt, const uint64_t* tab, uint32_t tbits,
-                        const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis, const uint8_t* dead,
-                        uint64_t r, uint64_t n, uint32_t W, Cand* cand, uint64_t cand_cap,
+hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
+                        uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis,
+                        const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand, uint64_t cand_cap,
                         unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
   const uint64_t waves = (nwt + kProbeWT - 1) / kProbeWT;
-  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(waves * 64, 256)), dim3(256), 0, s, data, av, nwt, tab, tbits,
-                     gfilt, anc_off, vis, dead, r, n, W, cand, cand_cap, counters);
+  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(waves * 64, 256)), dim3(256), 0, s, data, av, wt0, nwt, tab,
+                     tbits, gfilt, anc_off, vis, dead, r, p_end, W, cand, cand_cap, counters);
   return hipGetLastError();
 }
 
@@ -1759,12 +1760,12 @@ hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, ui
 template <int Q>
 static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, const uint8_t* data, uint64_t n,
                                         const uint64_t* blk, uint32_t W, uint32_t pw32, uint32_t sbyte,
-                                        uint64_t p_start, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* fmap,
+                                        uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, FKeys K, const uint32_t* fmap,
                                         Run* runs, uint64_t runs_cap, uint64_t* wt_off, uint32_t* wt_cnt,
                                         unsigned long long* counters) {
 #define ZC_FS(NF)                                                                                                  \
   hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(ZC_FTPB), 0, s, data, n, blk, W, pw32,     \
-                     sbyte, p_start, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
+                     sbyte, p_start, p_end, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
   if (nfk == 1) ZC_FS(1);
   else if (nfk == 4) ZC_FS(4);
   else ZC_FS(0);
@@ -1773,11 +1774,11 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
 }
 
 hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
-                               uint64_t p_start, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
+                               uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
                                uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
                                uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
-  if (W < 32 || n < 64 || (wt0 + nwt - 1) * ZC_FWT >= n || nf == 0) return hipErrorInvalidValue;
+  if (W < 32 || n < 64 || p_end > n || (wt0 + nwt - 1) * ZC_FWT >= p_end || nf == 0) return hipErrorInvalidValue;
   FKeys K;
   const int nfk = nf == 1 ? 1 : nf <= 4 ? 4 : 0;
   for (int i = 0; i < 4; ++i) K.k[i] = (nfk != 0 ? keys32[i < (int)nf ? i : 0] : 0u) - pw32;
@@ -1785,13 +1786,13 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
   const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * (ZC_FTPB / 64));
   const unsigned grid = (waves + ZC_FTPB / 64 - 1) / (ZC_FTPB / 64);
   switch (m >> 2) {
-    case 0: return launch_fscan_staged_q<0>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+    case 0: return launch_fscan_staged_q<0>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K, fbits17,
                                             runs, runs_cap, wt_off, wt_cnt, counters);
-    case 1: return launch_fscan_staged_q<1>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+    case 1: return launch_fscan_staged_q<1>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K, fbits17,
                                             runs, runs_cap, wt_off, wt_cnt, counters);
-    case 2: return launch_fscan_staged_q<2>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K, fbits17,
+    case 2: return launch_fscan_staged_q<2>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K, fbits17,
                                             runs, runs_cap, wt_off, wt_cnt, counters);
-    default: return launch_fscan_staged_q<3>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, wt0, nwt, K,
+    default: return launch_fscan_staged_q<3>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                              fbits17, runs, runs_cap, wt_off, wt_cnt, counters);
   }
 }
