@@ -196,15 +196,6 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// acc += {lo, hi} as ONE v_lshl_add_u64 (written as a 64-bit add of a bit-cast
-// pair; hipcc splits `acc + ((uint64_t)hi << 32 | lo)` into two adds + moves)
-__device__ __forceinline__ void add64_pair(uint32_t& hlo, uint32_t& hhi, uint32_t lo, uint32_t hi) {
-  const v2u32 a = {hlo, hhi}, t = {lo, hi};
-  const uint64_t r = __builtin_bit_cast(uint64_t, a) + __builtin_bit_cast(uint64_t, t);
-  hlo = (uint32_t)r;
-  hhi = (uint32_t)(r >> 32);
-}
-
 // One 16-byte piece of the scan (four dwords).  Gear: position k of a dword is
 // g_k = (g << (k+1)) + sum_{j<=k} b_j 2^(k-j), the byte-weighted sums coming
 // from v_dot4_u32_u8, so the four positions are independent of each other.
@@ -236,7 +227,10 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
 #pragma unroll
       for (int k = 0; k < 4; ++k) g[d][k] = (s.glo << (k + 1)) + dd[k];
       s.glo = g[d][3];
-      mx[d] = max(max((int32_t)g[d][0], (int32_t)g[d][1]), max((int32_t)g[d][2], (int32_t)g[d][3]));
+      // one max3 chain over the piece's 16 gears (8 v_max3_i32 per piece)
+      mx[d] = d == 0 ? max(max((int32_t)g[0][0], (int32_t)g[0][1]), (int32_t)g[0][2])
+                     : max(max(mx[d - 1], (int32_t)g[d - 1][3]), (int32_t)g[d][0]);
+      if (d > 0) mx[d] = max(max(mx[d], (int32_t)g[d][1]), (int32_t)g[d][2]);
     }
     if (!(ABL & ABL_NO_DIGEST)) {
       // two bytes per Horner step: acc*257^2 + (257 b_0 + b_1).  One v_perm
@@ -247,14 +241,17 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
       const uint32_t t[2] = {(sp & 0xFFFFu) + (x & 0xFFu), (sp >> 16) + ((x >> 16) & 0xFFu)};
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        const uint64_t R = (uint64_t)s.hlo * 66049u + t[k];
-        s.hhi = (uint32_t)((uint64_t)s.hhi * 66049u + (uint32_t)(R >> 32));
+        // acc*66049 + t = lo*66049 + {t, hi*66049}: a v_mul_lo_u32 for the
+        // high word feeds the 64-bit addend of ONE v_mad_u64_u32
+        const v2u32 addend = {t[k], s.hhi * 66049u};
+        const uint64_t R = (uint64_t)s.hlo * 66049u + __builtin_bit_cast(uint64_t, addend);
+        s.hhi = (uint32_t)(R >> 32);
         s.hlo = (uint32_t)R;
       }
     }
   }
   if (ABL & ABL_NO_GEAR) return;
-  const int32_t m = max(max(mx[0], mx[1]), max(mx[2], mx[3]));
+  const int32_t m = max(mx[3], (int32_t)g[3][3]);
   if (ABL & ABL_NO_BRANCH) {
     s.hhi ^= (uint32_t)m;
     return;
