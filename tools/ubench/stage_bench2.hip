@@ -8,6 +8,7 @@
 //   C  persistent coalesced register loads, 8 x dwordx4 per lane per round,
 //      one round in flight ahead
 //   D  grid-stride coalesced (non-persistent), 4 loads in flight
+//   E  4 KiB rows, each row's rounds rotated by (row % ROT) * 4096 / ROT bytes
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -24,7 +25,7 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 template <int N> __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // ROWSTRIDE: byte distance of consecutive rows (lanes); SPAN: bytes per row per tile
-template <int TPB, int ROWB, int SLOTS, int EXTRA, bool CONTIG, int S = 4096>
+template <int TPB, int ROWB, int SLOTS, int EXTRA, bool CONTIG, int S = 4096, int ROT = 1>
 __global__ void __launch_bounds__(TPB, 1) stage_kernel(const uint8_t* __restrict__ data, uint64_t ntiles, uint32_t* out) {
   constexpr int RPI = 1024 / ROWB;
   constexpr int NI = 64 / RPI;
@@ -45,7 +46,7 @@ __global__ void __launch_bounds__(TPB, 1) stage_kernel(const uint8_t* __restrict
       const uint32_t row = j * RPI + lane / PIECES;
       const uint32_t p = (lane % PIECES) ^ swz(row);
       const uint64_t wbase = tile * (uint64_t)(TPB * S) + (uint64_t)wave * 64 * S;
-      const uint64_t off = CONTIG ? (uint64_t)r * 64 * ROWB + (uint64_t)row * ROWB : (uint64_t)row * S + r * ROWB;
+      const uint64_t off = CONTIG ? (uint64_t)r * 64 * ROWB + (uint64_t)row * ROWB : (uint64_t)row * S + ((r * ROWB + ((wave * 64 + row) % ROT) * (S / ROT)) % S);
       __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wbase + off + p * 16), (lds_void_t*)(slot + j * 1024), 16, 0, 0);
     }
   };
@@ -143,6 +144,9 @@ int main() {
 #define STS(S) vs.push_back({"stage tpb=512 rowb=128 slots=2 stride=" #S, [=] { \
     uint64_t nt = n / (512 * (uint64_t)S); hipLaunchKernelGGL((stage_kernel<512, 128, 2, 0, false, S>), dim3(std::min<uint64_t>(nt, (uint64_t)cus)), dim3(512), 0, 0, d, nt, out); }, {}});
   STS(256) STS(512) STS(1024) STS(2048) STS(4096) STS(8192)
+#define STR(ROT) vs.push_back({"stage tpb=512 rowb=128 slots=2 stride=4096 rot=" #ROT, [=] { \
+    uint64_t nt = n / (512 * 4096ull); hipLaunchKernelGGL((stage_kernel<512, 128, 2, 0, false, 4096, ROT>), dim3(std::min<uint64_t>(nt, (uint64_t)cus)), dim3(512), 0, 0, d, nt, out); }, {}});
+  STR(2) STR(4) STR(8) STR(32)
 #define REG(TPB, DEPTH, EXTRA, WPC) vs.push_back({"reg tpb=" #TPB " depth=" #DEPTH " extra=" #EXTRA " wg/cu=" #WPC, [=] { \
     hipLaunchKernelGGL((reg_kernel<TPB, DEPTH, EXTRA>), dim3(cus * WPC), dim3(TPB), 0, 0, d, n / 8192, out); }, {}});
   REG(512, 2, 0, 1)

@@ -35,6 +35,23 @@ KERNEL32(k_bfe, "v_bfe_u32 %0, %0, 8, 8")
 KERNEL32(k_pk_add, "v_pk_add_u16 %0, %0, %1")
 KERNEL32(k_sad, "v_sad_u8 %0, %0, %1, %2")
 KERNEL32(k_lerp, "v_lerp_u8 %0, %0, %1, %2")
+KERNEL32(k_and, "v_and_b32 %0, %0, %1")
+KERNEL32(k_or, "v_or_b32 %0, %0, %1")
+KERNEL32(k_xor, "v_xor_b32 %0, %0, %1")
+KERNEL32(k_max, "v_max_i32 %0, %0, %1")
+KERNEL32(k_lshlrev, "v_lshlrev_b32 %0, 3, %0")
+KERNEL32(k_add_sdwa, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2")
+KERNEL32(k_add3, "v_add3_u32 %0, %0, %1, %2")
+KERNEL32(k_or3, "v_or3_b32 %0, %0, %1, %2")
+KERNEL32(k_lshl_or, "v_lshl_or_b32 %0, %0, 2, %1")
+KERNEL32(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+KERNEL32(k_mad_u16, "v_mad_u32_u16 %0, %0, %1, %2")
+KERNEL32(k_dot2, "v_dot2_u32_u16 %0, %0, %1, %2")
+KERNEL32(k_mul_hi, "v_mul_hi_u32 %0, %0, %1")
+KERNEL32(k_pk_mad, "v_pk_mad_u16 %0, %0, %1, %2")
+KERNEL32(k_pk_fma, "v_pk_fma_f16 %0, %0, %1, %2")
+KERNEL32(k_fma, "v_fma_f32 %0, %0, %1, %2")
+KERNEL32(k_cvt_pk, "v_cvt_pk_u8_f32 %0, %1, 1, %0")
 
 #define KERNEL64(NAME, ASM)                                                               \
   __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed) {             \
@@ -75,6 +92,12 @@ int main() {
             {"v_alignbit_b32", k_alignbit, 1}, {"v_dot4_u32_u8", k_dot4, 1}, {"v_mul_lo_u32", k_mul_lo, 1},
             {"v_mul_u32_u24", k_mul24, 1}, {"v_mad_u32_u24", k_mad24, 1}, {"v_max3_i32", k_max3, 1},
             {"v_bfe_u32", k_bfe, 1}, {"v_pk_add_u16", k_pk_add, 1}, {"v_sad_u8", k_sad, 1}, {"v_lerp_u8", k_lerp, 1},
+            {"v_and_b32", k_and, 1}, {"v_or_b32", k_or, 1}, {"v_xor_b32", k_xor, 1}, {"v_max_i32", k_max, 1},
+            {"v_lshlrev_b32", k_lshlrev, 1}, {"v_add_u32_sdwa", k_add_sdwa, 1}, {"v_add3_u32", k_add3, 1},
+            {"v_or3_b32", k_or3, 1}, {"v_lshl_or_b32", k_lshl_or, 1}, {"v_add_u32_e64", k_add_e64, 1},
+            {"v_mad_u32_u16", k_mad_u16, 1}, {"v_dot2_u32_u16", k_dot2, 1}, {"v_mul_hi_u32", k_mul_hi, 1},
+            {"v_pk_mad_u16", k_pk_mad, 1}, {"v_pk_fma_f16", k_pk_fma, 1}, {"v_fma_f32", k_fma, 1},
+            {"v_cvt_pk_u8_f32", k_cvt_pk, 1},
             {"v_lshl_add_u64", k_lshl_add64, 1},
             {"v_mad_u64_u32", k_mad64, 1}};
   const int blocks = cus * 8, tpb = 256;

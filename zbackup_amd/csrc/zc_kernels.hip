@@ -375,9 +375,18 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-constexpr int kRounds = ZC_LSPAN / ZC_ROUND;  // rounds per tile (plus one warm-up round)
+constexpr int kRounds = ZC_LSPAN / ZC_ROUND;  // rounds per tile
 constexpr int kDmaRound = 64 * ZC_ROUND / 1024;  // DMA instructions per wave-round
 constexpr int kDigests = ZC_LSPAN / ZC_SPAN;     // span digests per lane span
+// Odd rows (lanes) take their lane span's two halves in the other order
+// (round r reads half-span-rotated round r ^ kHalfRounds): the rows of a
+// wave-round are then not all 4 KiB apart, a stride that costs the staging
+// 12 % (tools/ubench/stage_bench2.hip: 5.5 -> 6.3 TB/s staged).  The gear is
+// re-primed from the 32 bytes before each half, so a lane's anchors and gear
+// values do not depend on the order.
+constexpr int kHalfRounds = kRounds / 2;
+constexpr uint32_t kHalfSpan = ZC_LSPAN / 2;
+static_assert((kHalfRounds & (kHalfRounds - 1)) == 0 && kHalfRounds % (ZC_SPAN / ZC_ROUND) == 0, "half-span rotation");
 
 // LDS image of a wave-round: row i (lane i's ZC_ROUND bytes) is stored
 // linearly, with its 16-byte piece p at position p ^ swz(i); the swizzle makes
@@ -387,7 +396,8 @@ constexpr int kPieces = ZC_ROUND / 16;
 __host__ __device__ constexpr uint32_t row_swizzle(uint32_t row) { return (row / (256 / ZC_ROUND)) % kPieces; }
 
 // DMA of round r of `tile` into ring slot `slot`: ZC_ROUND bytes of each of
-// the wave's 64 rows; one instruction fills 1024 / ZC_ROUND rows (1 KiB).
+// the wave's 64 rows (an odd row's from the other half of its span); one
+// instruction fills 1024 / ZC_ROUND rows (1 KiB).
 // Through a buffer descriptor at the wave-round's first byte (wave-uniform,
 // built with scalar instructions): the lane's part of every instruction is
 // its loop-invariant 32-bit offset lane_off[j], so a round costs no vector
@@ -396,11 +406,13 @@ __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, ui
                                             const uint32_t (&lane_off)[kDmaRound], uint64_t tile, int r,
                                             uint32_t slot) {
   uint8_t* dst = ring + slot * (64 * ZC_ROUND);
-  const uint64_t at = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)r * ZC_ROUND;
+  const uint64_t at = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)(r % kHalfRounds) * ZC_ROUND;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(data + at), (short)0, 64 * ZC_LSPAN, 0x00020000);
+  const uint32_t flip = r >= kHalfRounds ? kHalfSpan : 0u;
 #pragma unroll
   for (int j = 0; j < kDmaRound; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + j * 1024), 16, (int)lane_off[j], 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + j * 1024), 16, (int)(lane_off[j] ^ flip), 0, 0,
+                                             0);
 }
 
 template <int N>
@@ -520,17 +532,23 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   uint32_t tot = 0, excl = 0;
   bool over = wl.n > ZC_WLIST;
   if (!over) {
-    uint32_t cnt = 0;
-    for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu)
-      cnt += __popc(piece_hits(wl, i, span0, lo_thr).mask);
+    uint32_t cnt = 0, cnt_lo = 0;  // cnt_lo: anchors in the span's first half
+    for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
+      const PieceHits h = piece_hits(wl, i, span0, lo_thr);
+      cnt += __popc(h.mask);
+      if (h.rel < kHalfSpan) cnt_lo += __popc(h.mask);
+    }
     excl = wave_excl_scan(cnt, lane, &tot);
     over = tot > po.wcap;
     if (!over) {
-      // newest entry first: its anchors end at excl + cnt
+      // newest entry first, within each half: the first half's anchors end at
+      // excl + cnt_lo, the second half's at excl + cnt (either half may be the
+      // one taken first)
       const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
-      uint32_t k = base + excl + cnt;
+      uint32_t k_lo = base + excl + cnt_lo, k_hi = base + excl + cnt;
       for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
         const PieceHits h = piece_hits(wl, i, span0, lo_thr);
+        uint32_t& k = h.rel < kHalfSpan ? k_lo : k_hi;
         k -= __popc(h.mask);
         uint32_t g = h.g0, w = k;
         for (uint32_t t = 0; t < 16; ++t) {
@@ -556,9 +574,9 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
 // tile).  A round is read from its ring slot into registers first; the slot
 // is then refilled with the round two ahead before the round is hashed, so
 // two rounds (16 KiB per wave) are in flight while a wave computes.  The 32
-// bytes before each lane span (they prime the gear) are two per-lane register
-// loads issued together with the DMA of the tile's first round, so tile
-// boundaries cost no extra pipeline round.
+// bytes before each half of a lane span (they prime the gear) are two
+// per-lane register loads issued together with the DMA of the half's first
+// round, so half and tile boundaries cost no extra pipeline round.
 template <int ABL>
 __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
@@ -579,17 +597,18 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
 #pragma unroll
   for (int j = 0; j < kDmaRound; ++j) {
     const uint32_t row = j * (1024 / ZC_ROUND) + lane / kPieces;
-    lane_off[j] = row * ZC_LSPAN + ((lane % kPieces) ^ row_swizzle(row)) * 16;
+    lane_off[j] = row * ZC_LSPAN + (row & 1) * kHalfSpan + ((lane % kPieces) ^ row_swizzle(row)) * 16;
   }
   const uint32_t sw = row_swizzle(lane);  // read-side swizzle of this lane's row
-  v4u32 warm[2];                          // the 32 bytes before the next tile's span
+  const uint32_t hs = (lane & 1) * kHalfRounds;  // logical round r is physical round r ^ hs
+  v4u32 warm[2];                          // the 32 bytes before the next half span
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kRpt, r = Rx - k * kRpt;
     const uint64_t tile = tile0 + blockIdx.x + (uint64_t)k * grid;
     stage_round(data, myring, wave, lane_off, tile, (int)r, Rx & 1);
-    if (r == 0) {
+    if (r % kHalfRounds == 0) {
       // span 0 of the stream has no bytes before it: it reads itself (unused)
-      const uint64_t at = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
+      const uint64_t at = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN + (uint64_t)(r ^ hs) * ZC_ROUND;
       const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
       warm[0] = global_read16(src);
       warm[1] = global_read16(src + 16);
@@ -609,23 +628,29 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   for (uint32_t R = 0; R < nR; ++R) {
     const uint32_t k = R / kRpt;
     const int r = (int)(R - k * kRpt);
-    // round R (and, for a tile's first round, its warm-up loads) has landed
+    // round R (and, for a half's first round, its warm-up loads) has landed
     // once only what was issued after it is outstanding: round R + 1's DMA,
-    // plus the next tile's warm-up loads after round kRounds - 2, plus the
-    // tile end's stores before round 0
+    // plus the next half's warm-up loads before a half's first round, plus
+    // the tile end's stores before round 0
     if (R + 1 >= nR) wait_vmcnt<0>();
-    else if (r == kRounds - 1) wait_vmcnt<kDmaRound + 2>();
+    else if ((r + 1) % kHalfRounds == 0) wait_vmcnt<kDmaRound + 2>();
     else if (r == 0) wait_vmcnt_dyn(kDmaRound + tail_stores);
     else wait_vmcnt<kDmaRound>();
     const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND);
+    const uint32_t pr = (uint32_t)r ^ hs;  // the physical round in the lane span
     if (r == 0) {
-      // a new tile: the warm-up bytes prime the gear
+      // a new tile
       span0 = (tile0 + blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
       s = ScanLane{0, 0, 0};
       wl.n = 0;
       last = kNoEntry;
+    }
+    if (r % kHalfRounds == 0) {
+      // a new half: the warm-up bytes prime the gear (its value depends on the
+      // 32 bytes before only, so this equals the gear rolled on continuously)
+      s.glo = 0;
       ties(warm);  // landed: the wait above covers them
-      if (span0 >= 64) {
+      if (span0 + pr * ZC_ROUND >= 64) {
         const uint32_t xs[8] = {warm[0][0], warm[0][1], warm[0][2], warm[0][3],
                                 warm[1][0], warm[1][1], warm[1][2], warm[1][3]};
 #pragma unroll
@@ -644,13 +669,12 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     for (int p = 0; p < kPieces; ++p) v[p] = to_uint4(vr[p]);
     if (R + 2 < nR) issue(R + 2);
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], (uint32_t)r * ZC_ROUND + p * 16, lo_thr, s, wl, last);
+    for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
-      const int q = r / (ZC_SPAN / ZC_ROUND);
+      const uint32_t q = pr / (ZC_SPAN / ZC_ROUND);  // per lane: the halves are rotated
 #pragma unroll
-      for (int t = 0; t < kDigests; ++t)
-        if (q == t) bk[t] = h;
+      for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
     if (r == kRounds - 1 && !(ABL & ABL_NO_TILE_END))
