@@ -40,7 +40,7 @@ int main(int argc, char** argv) {
     {"full_never_taken", zc_scan_kernel<ABL_NEVER>, {}},
     {"gear_never_taken", zc_scan_kernel<ABL_NEVER | ABL_NO_DIGEST>, {}},
   };
-  for (int round = 0; round < 6; ++round)
+  for (int round = 0; round < 12; ++round)
     for (auto& v : vs) {
       CK(hipMemset(cnt, 0, 64));
       CK(hipEventRecord(a));

@@ -138,37 +138,50 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
                                 const uint32_t* sbase, uint32_t ntiles, int pass, uint32_t* base, uint32_t* cnt,
                                 uint32_t* srel, uint32_t* sg, hipStream_t s);
 
-// grid chunks i < nchunks of an epoch starting at r_e (start = r_e + i * W)
-hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
-                             uint32_t nchunks, uint32_t W, uint64_t pw, uint64_t* start, uint64_t* vis,
-                             uint8_t* dead, uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off,
-                             hipStream_t s);
-
-hipError_t launch_anchorless(const uint32_t* anc_off, const uint32_t* cls, uint32_t nref, uint32_t* list,
-                             uint32_t cap, unsigned long long* counters, hipStream_t s);
-
-// content classes of refs [0, nref): cls[i] = lowest ref with an equal key and
-// equal bytes (counters[CNT_CLASS] += refs that are not leaders); the class
-// table has 2^cbits >= 2 nref slots
-hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64_t* start, uint32_t nref, uint32_t W,
-                          uint64_t* ckeys, uint32_t* cvals, uint32_t cbits, uint32_t* cls,
-                          unsigned long long* counters, hipStream_t s);
-
-hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s);
-// table of class leaders' first anchors (2^tbits slots of 16 bytes: 2 << tbits
-// words of tab) and its key filter gfilt (probe_filter_words() words); both
-// cleared and filled here
-hipError_t launch_table_insert(uint64_t* tab, uint32_t tbits, const uint32_t* cg, const uint64_t* cfp,
-                               const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs, uint32_t* gfilt,
-                               hipStream_t s);
+// The device side of an epoch's index, three launches:
+//   1. grid chunks i < nsref starting at r_e + i * W (refs nconf + i): start,
+//      visibility, key, first anchor {offset, gear, fingerprint}; and every
+//      table and counter below cleared;
+//   2. per ref: the content-class table (lowest ref per key) and, for refs
+//      with an anchor, the anchor table {gear | ref << 32, fingerprint} and
+//      its key filter;
+//   3. per ref: cls = the lowest ref with an equal key whose bytes are equal
+//      (else itself; counters[CNT_CLASS] += refs that are not leaders), and
+//      the class leaders without an anchor listed at ancless
+//      (counters[CNT_ANCLESS]).
+// Refs [0, nconf) must have start/key/cg/cfp/anc uploaded (vis = 0, dead = 0).
+// The class table has 2^cbits >= 2 nref slots, the anchor table 2^tbits
+// (2 << tbits words of tab; tab may be null when the stream has no anchors).
+struct EpochIndex {
+  uint64_t* start;
+  uint64_t* vis;
+  uint8_t* dead;
+  uint64_t* key;
+  uint32_t* cg;
+  uint64_t* cfp;
+  uint32_t* anc;
+  uint32_t* cls;
+  uint64_t* ckeys;
+  uint32_t* cvals;
+  uint32_t cbits;
+  uint64_t* tab;
+  uint32_t tbits;
+  uint32_t* gfilt;
+  uint32_t* ancless;
+  unsigned long long* counters;
+};
+hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
+                              uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
+                              hipStream_t s);
 uint32_t probe_filter_words();
 
 // every anchor of wave-tiles [wt0, wt0 + nwt) probes the filter, then the
 // table; candidate windows start at >= r (the reset point) and end before p_end
+// (the table holds every ref with an anchor; candidates name class leaders)
 hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
-                        uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis,
-                        const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand, uint64_t cand_cap,
-                        unsigned long long* counters, hipStream_t s);
+                        uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint32_t* cls,
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand,
+                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,

@@ -131,7 +131,30 @@ constexpr size_t kFBatchMax = 1u << 20;
 constexpr uint64_t kHostSegment = 64ull << 20;  // zc_chunk_host copy/scan pipeline granularity
 constexpr uint64_t kHorizon0 = 256ull << 10;    // first horizon of an epoch after a grid shift (>= 64 W)
 
+// an allocator whose value construction is default-initialisation: growing a
+// vector of plain records does not zero memory that is written right after
+// (the record writes are the host's share of a stream: ~5 MB per 8 GiB)
+template <class T>
+struct DefaultInit : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInit<U>;
+  };
+  DefaultInit() = default;
+  template <class U>
+  DefaultInit(const DefaultInit<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+
 }  // namespace
+
 
 struct zc_ctx {
   int device = 0;
@@ -139,7 +162,7 @@ struct zc_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_in = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_in = nullptr, ev_idx = nullptr;
   std::string err;
 
   // host feed
@@ -151,7 +174,7 @@ struct zc_ctx {
   uint64_t n_last = 0;
 
   std::vector<StaticEntry> statics;  // seeded index entries of size W
-  std::vector<zc_record> recs;
+  std::vector<zc_record, DefaultInit<zc_record>> recs;  // resize leaves new records to be written
   zc_stats stats{};
 
   // scratch
@@ -474,39 +497,43 @@ class Resolver {
         HCK(hipMemsetAsync(c_.c_vis.p, 0, nconf_ * sizeof(uint64_t), c_.stream));
         HCK(hipMemsetAsync(c_.c_dead.p, 0, nconf_, c_.stream));
       }
-      HCK(launch_chunk_meta(d_, n_, c_.blk.p, av_, r_e_, nsref, W_, pow257(W_), c_.c_start.p + nconf_,
-                            c_.c_vis.p + nconf_, c_.c_dead.p + nconf_, c_.c_key.p + nconf_,
-                            c_.c_g.p + nconf_, c_.c_fp.p + nconf_, c_.c_anc.p + nconf_, c_.stream));
-      HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
       uint32_t tbits = 10;  // sized for every ref having an anchor
       while ((1u << tbits) < 2u * nref_) ++tbits;
       // content classes: identical refs share one leader in the table
       c_.ckeys.ensure(1u << tbits);
       c_.cvals.ensure(1u << tbits);
       c_.c_cls.ensure(nref_);
-      HCK(launch_classes(d_, c_.c_key.p, c_.c_start.p, nref_, W_, c_.ckeys.p, c_.cvals.p, tbits, c_.c_cls.p,
-                         c_.counters.p, c_.stream));
       if (npool_) {
         c_.tab.ensure(2u << tbits);
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         c_.gfilt.ensure(probe_filter_words());
-        HCK(launch_table_insert(c_.tab.p, tbits, c_.c_g.p, c_.c_fp.p, c_.c_anc.p, c_.c_cls.p, nref_, c_.gfilt.p,
-                                c_.stream));
-        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p,
-                         c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       }
-      HCK(launch_anchorless(c_.c_anc.p, c_.c_cls.p, nref_, c_.ancless.p, nref_, c_.counters.p, c_.stream));
-      d2h(c_, c_.h_key.p, c_.c_key.p + nconf_, nsref);
+      const EpochIndex ix{c_.c_start.p, c_.c_vis.p,  c_.c_dead.p, c_.c_key.p, c_.c_g.p,
+                          c_.c_fp.p,    c_.c_anc.p,  c_.c_cls.p,  c_.ckeys.p, c_.cvals.p,
+                          tbits,        npool_ ? c_.tab.p : nullptr, tbits, c_.gfilt.p, c_.ancless.p,
+                          c_.counters.p};
+      HCK(launch_epoch_index(d_, n_, c_.blk.p, av_, r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
+      // the grid chunks' keys go to the host on the side stream while the
+      // probe runs
+      HCK(hipEventRecord(c_.ev_idx, c_.stream));
+      HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
+      if (nsref)
+        HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                           c_.copy_stream));
+      if (npool_)
+        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
+      HCK(hipStreamSynchronize(c_.copy_stream));
       ncand = c_.h_cnt[CNT_CAND];
       nancless = c_.h_cnt[CNT_ANCLESS];
       if (c_.h_cnt[CNT_CLASS]) load_classes();
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_vis.p,
-                         c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
         ncand = c_.h_cnt[CNT_CAND];
@@ -955,21 +982,30 @@ class Resolver {
   }
 
   // save the grid chunks of this epoch whose cut happens at or before probe m
+  // (chunk k is cut at r_e + (k+2)W - 1); the records are written in place,
+  // the common case being every grid chunk of the stream at once
   void save_grid_until(uint64_t m) {
-    while (ks_ < nspec_) {
-      const uint64_t ck = r_e_ + ks_ * W_;
-      if (ck + 2ull * W_ - 1 > m) break;
-      const bool dead = indexable_ && dead_[nconf_ + ks_];
-      if (!dead && ck >= s_) {
-        if (indexable_) {
-          push(ck, W_, ZC_CHUNK_NEW, c_.h_key[ks_]);
-        } else {
-          push(ck, W_, ZC_BYTES, 0);
-        }
-        s_ = ck + W_;
-      }
-      ++ks_;
+    if (ks_ >= nspec_ || r_e_ + 2ull * W_ - 1 > m) return;
+    const uint64_t kmax = std::min<uint64_t>(nspec_, (m - (r_e_ + 2ull * W_ - 1)) / W_ + 1);
+    if (ks_ >= kmax) return;
+    size_t o = c_.recs.size();
+    c_.recs.resize(o + (kmax - ks_));
+    zc_record* rec = c_.recs.data();
+    const uint32_t kind = indexable_ ? (uint32_t)ZC_CHUNK_NEW : (uint32_t)ZC_BYTES;
+    const uint8_t* dead = indexable_ ? dead_.data() + nconf_ : nullptr;
+    for (uint64_t k = ks_; k < kmax; ++k) {
+      const uint64_t ck = r_e_ + k * W_;
+      if ((dead && dead[k]) || ck < s_) continue;
+      zc_record& r = rec[o++];
+      r.offset = ck;
+      r.size = W_;
+      r.kind = kind;
+      r.rolling = indexable_ ? c_.h_key[k] : 0;
+      memset(r.sha1, 0, sizeof r.sha1);
+      s_ = ck + W_;
     }
+    c_.recs.resize(o);
+    ks_ = kmax;
   }
 
   void finish() {
@@ -1186,6 +1222,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreate(&c->ev0));
     HCK(hipEventCreate(&c->ev1));
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
   if (rc != ZC_OK) {
@@ -1207,6 +1244,7 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);

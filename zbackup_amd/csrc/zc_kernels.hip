@@ -453,16 +453,20 @@ __device__ __forceinline__ void ties(v4u32 (&v)[N]) {
   }
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n < 40 (the tile end's store count is
-// only known at run time)
+// s_waitcnt vmcnt(n) for a wave-uniform n (the tile end's store count is only
+// known at run time); n < 8 or n > 63 waits for fewer, which is always safe
 __device__ __forceinline__ void wait_vmcnt_dyn(uint32_t n) {
   switch (n) {
 #define ZC_W(k) case k: wait_vmcnt<k>(); break;
     ZC_W(8) ZC_W(9) ZC_W(10) ZC_W(11) ZC_W(12) ZC_W(13) ZC_W(14) ZC_W(15) ZC_W(16) ZC_W(17) ZC_W(18)
     ZC_W(19) ZC_W(20) ZC_W(21) ZC_W(22) ZC_W(23) ZC_W(24) ZC_W(25) ZC_W(26) ZC_W(27) ZC_W(28) ZC_W(29)
-    ZC_W(30) ZC_W(31) ZC_W(32) ZC_W(33) ZC_W(34) ZC_W(35) ZC_W(36) ZC_W(37) ZC_W(38) ZC_W(39)
+    ZC_W(30) ZC_W(31) ZC_W(32) ZC_W(33) ZC_W(34) ZC_W(35) ZC_W(36) ZC_W(37) ZC_W(38) ZC_W(39) ZC_W(40)
+    ZC_W(41) ZC_W(42) ZC_W(43) ZC_W(44) ZC_W(45) ZC_W(46) ZC_W(47) ZC_W(48) ZC_W(49) ZC_W(50) ZC_W(51)
+    ZC_W(52) ZC_W(53) ZC_W(54) ZC_W(55) ZC_W(56) ZC_W(57) ZC_W(58) ZC_W(59) ZC_W(60) ZC_W(61) ZC_W(62)
 #undef ZC_W
-    default: wait_vmcnt<0>();
+    default:
+      if (n > 62) wait_vmcnt<63>();
+      else wait_vmcnt<0>();
   }
 }
 
@@ -513,15 +517,31 @@ __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, 
 // entry and the anchor count.  Every lane walks only its own entries (a chain
 // through the list, newest first, `last` = its newest): once to count, once
 // to store, so the list costs O(entries per lane), not O(entries).  Returns a
-// lower bound of the global stores it leaves in flight (the digests, the
-// directory pair, the count) so the next round's wait can leave them be.  A
-// wave-tile whose list or pool share overflowed is marked for the exact
-// rescan (zc_anchor_rescan) and stores no anchors.
+// lower bound of the global stores it leaves in flight, so the next round's
+// wait can leave them be.  The anchors go through `stage` (the wave's ring
+// slot of the round just read, free until the next DMA is issued): each lane
+// writes its own there, then the wave stores them with ceil(tot / 64)
+// coalesced store pairs -- a count the wave knows, so the bound is exact and
+// the next round's wait does not drain the prefetch.  (More anchors than the
+// slot holds are stored straight from the lanes and the bound is only a
+// lower one.)  A wave-tile whose list or pool share overflowed is marked for
+// the exact rescan (zc_anchor_rescan) and stores no anchors.
+constexpr uint32_t kStageAnchors = 64 * ZC_ROUND / 8;  // {rel, gear} per anchor
+__device__ __forceinline__ void lds_write32(uint8_t* p, uint32_t v) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)p;
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_read32(const uint8_t* p) {
+  uint32_t v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
 template <int ABL>
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
                                                   const uint64_t (&bk)[kDigests], const WaveList& wl,
-                                                  uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
-                                                  unsigned long long* __restrict__ counters) {
+                                                  uint32_t last, uint8_t* stage, uint64_t* __restrict__ blk,
+                                                  PoolOut po, unsigned long long* __restrict__ counters) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
 #pragma unroll
   for (int t = 0; t < kDigests / 2; ++t)
@@ -529,7 +549,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
                        (uint32_t)(bk[2 * t + 1] >> 32));
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)wt * po.wcap;
-  uint32_t tot = 0, excl = 0;
+  uint32_t tot = 0, excl = 0, nst = kDigests / 2 + 2 + ((ABL & ABL_NO_ATOMIC) ? 0 : 1);
   bool over = wl.n > ZC_WLIST;
   if (!over) {
     uint32_t cnt = 0, cnt_lo = 0;  // cnt_lo: anchors in the span's first half
@@ -539,13 +559,15 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
       if (h.rel < kHalfSpan) cnt_lo += __popc(h.mask);
     }
     excl = wave_excl_scan(cnt, lane, &tot);
+    tot = __builtin_amdgcn_readfirstlane(tot);
     over = tot > po.wcap;
     if (!over) {
+      const bool staged = tot <= kStageAnchors;
       // newest entry first, within each half: the first half's anchors end at
       // excl + cnt_lo, the second half's at excl + cnt (either half may be the
       // one taken first)
       const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
-      uint32_t k_lo = base + excl + cnt_lo, k_hi = base + excl + cnt;
+      uint32_t k_lo = excl + cnt_lo, k_hi = excl + cnt;
       for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
         const PieceHits h = piece_hits(wl, i, span0, lo_thr);
         uint32_t& k = h.rel < kHalfSpan ? k_lo : k_hi;
@@ -554,11 +576,30 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
         for (uint32_t t = 0; t < 16; ++t) {
           g = (g << 1) + ((h.xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
           if ((h.mask >> t) & 1) {
-            po.rel[w] = rbase + h.rel + t;
-            po.g[w] = g;
+            if (staged) {
+              lds_write32(stage + 4 * w, rbase + h.rel + t);
+              lds_write32(stage + 4 * (kStageAnchors + w), g);
+            } else {
+              po.rel[base + w] = rbase + h.rel + t;
+              po.g[base + w] = g;
+            }
             ++w;
           }
         }
+      }
+      if (staged) {
+        wait_lgkmcnt<0>();  // the wave's writes landed (LDS ops of a wave complete in order)
+        const uint32_t nit = (tot + 63) / 64;  // wave-uniform: one store pair each
+        for (uint32_t it = 0; it < nit; ++it) {
+          const uint32_t i = it * 64 + lane;
+          if (i < tot) {
+            const uint32_t a = lds_read32(stage + 4 * i), b = lds_read32(stage + 4 * (kStageAnchors + i));
+            wait_lgkmcnt<0>();
+            po.rel[base + i] = a;
+            po.g[base + i] = b;
+          }
+        }
+        nst += 2 * nit;
       }
     }
   }
@@ -567,7 +608,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
     po.cnt[wt] = over ? ZC_WT_OVERFLOW : tot;
     if (!(ABL & ABL_NO_ATOMIC)) atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
   }
-  return kDigests / 2 + 3;
+  return nst;
 }
 
 // The workgroup's rounds form one flat sequence over its tiles (32 per
@@ -667,7 +708,10 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     uint4 v[kPieces];
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) v[p] = to_uint4(vr[p]);
-    if (R + 2 < nR) issue(R + 2);
+    // a tile's last round issues the DMA two ahead only after the tile end,
+    // which uses the slot just read to stage the anchors
+    const bool tile_end = r == kRounds - 1 && !(ABL & ABL_NO_TILE_END);
+    if (R + 2 < nR && !tile_end) issue(R + 2);
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
@@ -677,8 +721,11 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (r == kRounds - 1 && !(ABL & ABL_NO_TILE_END))
-      tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, counters);
+    if (tile_end) {
+      tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, (uint8_t*)row, blk, po, counters);
+      wait_lgkmcnt<0>();  // the staging reads are done before the DMA refills the slot
+      if (R + 2 < nR) issue(R + 2);
+    }
   }
 }
 
@@ -737,18 +784,40 @@ __device__ __forceinline__ TileAnchors tile_anchors(const AnchorView& av, uint64
 }
 
 // ---------------------------------------------------------------------------
+// the epoch's tables and counters, cleared by the chunk-metadata launch
+struct EpochClear {
+  uint64_t* ckeys;  // class table keys: empty
+  uint32_t* cvals;  // class table leaders: none
+  uint32_t cwords;
+  uint64_t* tab;  // anchor table: empty (null: none)
+  uint64_t twords;
+  uint32_t* gfilt;  // key filter: zero
+  uint32_t gwords;
+  unsigned long long* counters;
+};
+
 // zc_chunk_meta: thread per grid chunk i of the epoch, start = r_e + i * W:
 // start, visibility time, key, first anchor (offset, gear value, 64-byte
-// fingerprint); the chunk is not yet consumed by a match (dead = 0)
+// fingerprint); the chunk is not yet consumed by a match (dead = 0).  The
+// whole grid also clears the epoch's tables (no separate fills).
 __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
                                      const uint64_t* __restrict__ blk, AnchorView av, uint64_t r_e,
                                      uint32_t nchunks, uint32_t W, uint64_t pw,
                                      uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
                                      uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
-                                     uint32_t* __restrict__ anc_off) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nchunks) return;
+                                     uint32_t* __restrict__ anc_off, EpochClear ec) {
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = gt; j < ec.cwords; j += gs) {
+    ec.ckeys[j] = ~0ull;
+    ec.cvals[j] = ~0u;
+  }
+  if (ec.tab)
+    for (uint64_t j = gt; j < ec.twords; j += gs) ec.tab[j] = ~0ull;
+  for (uint64_t j = gt; j < ec.gwords; j += gs) ec.gfilt[j] = 0u;
+  if (gt < CNT_LAST) ec.counters[gt] = 0ull;
+  if (gt >= nchunks) return;
+  const uint32_t i = (uint32_t)gt;
   const uint64_t c = r_e + (uint64_t)i * W;
   start[i] = c;
   vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
@@ -783,26 +852,11 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   cfp[i] = f;
 }
 
-// class leaders without an anchor (they go through the exact-hash screen), compacted
-__global__ void zc_anchorless_kernel(const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
-                                     uint32_t nref, uint32_t* __restrict__ list, uint32_t cap,
-                                     unsigned long long* __restrict__ counters) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nref || anc_off[i] != ZC_NO_ANCHOR || cls[i] != i) return;
-  unsigned long long k = atomicAdd(&counters[CNT_ANCLESS], 1ull);
-  if (k < cap) list[k] = i;
-}
-
 // ---------------------------------------------------------------------------
 // anchor table: open addressing on the anchor's gear value, duplicates kept.
 // A slot is 16 bytes, {gear | ref << 32, fingerprint}: one load gives the
 // key, the ref and the fingerprint to compare (empty: all ones).
 constexpr uint64_t kEmpty = ~0ull;
-
-__global__ void zc_table_clear_kernel(uint64_t* tkeys, uint32_t tsize) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < tsize) tkeys[i] = kEmpty;
-}
 
 __device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
   return (uint32_t)(((uint64_t)g * kGolden) >> (64 - tbits));
@@ -813,27 +867,6 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
 constexpr int kGFiltBits = 20;                               // 2^20 bits = 128 KiB
 constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
 
-__global__ void zc_table_insert_kernel(uint64_t* tab, uint32_t tbits, const uint32_t* __restrict__ cg,
-                                       const uint64_t* __restrict__ cfp, const uint32_t* __restrict__ anc_off,
-                                       const uint32_t* __restrict__ cls, uint32_t nrefs, uint32_t* __restrict__ gfilt) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrefs || anc_off[i] == ZC_NO_ANCHOR || cls[i] != i) return;
-  const uint32_t fb = cg[i] & ((1u << kGFiltBits) - 1);
-  atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
-  const uint64_t word = ((uint64_t)i << 32) | cg[i];
-  const uint32_t mask = (1u << tbits) - 1;
-  uint32_t h = table_slot(cg[i], tbits);
-  for (;;) {
-    unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
-                                        (unsigned long long)word);
-    if (prev == kEmpty) {
-      tab[2 * (uint64_t)h + 1] = cfp[i];
-      return;
-    }
-    h = (h + 1) & mask;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // zc_probe: every anchor of the stream probes the table (key = gear value,
 // confirmed by the 64-byte fingerprint).  A wave takes kProbeWT consecutive
@@ -843,31 +876,33 @@ __global__ void zc_table_insert_kernel(uint64_t* tab, uint32_t tbits, const uint
 // The loads are issued level by level -- every slot's gear value, then every
 // filter word -- so a lane has all of them in flight at once; an anchor
 // tests the table's 2^20-bit key filter (L2 resident, ~1 in 8 pass at
-// W = 64 KiB) and only then walks the table.
+// W = 64 KiB) and only then walks the table.  The passing anchors of the
+// wave are compacted into LDS and walked one per lane, so the table walks
+// (a few dependent loads each) run side by side instead of one slot after
+// another.
 constexpr int kProbeWT = 2;     // wave-tiles per wave
 constexpr int kProbeSlots = 4;  // slots per lane per wave-tile (covers wcap <= 256)
+constexpr int kProbeTPB = 256;
 
 __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
                                              const uint64_t* __restrict__ tab, uint32_t tbits,
-                                             const uint32_t* __restrict__ anc_off, const uint64_t* __restrict__ vis,
-                                             const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W,
+                                             const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
+                                             const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead,
+                                             uint64_t r, uint64_t n, uint32_t W,
                                              Cand* __restrict__ cand, uint64_t cand_cap,
                                              unsigned long long* __restrict__ counters) {
   if (pos < r + ZC_ANCHOR_MIN_OFF) return;
   const uint32_t mask = (1u << tbits) - 1;
   uint32_t h = table_slot(gk, tbits);
-  bool have_fp = false;
-  uint64_t fp = 0;
+  // the filter passed, so the gear is almost surely in the table: the
+  // fingerprint loads go out together with the first slot's
+  const uint64_t fp = anchor_fp(data, pos);
   for (;;) {
     const uint4 slot = *(const uint4*)(tab + 2 * (uint64_t)h);
     if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
     if (slot.x == gk) {
-      if (!have_fp) {
-        fp = anchor_fp(data, pos);
-        have_fp = true;
-      }
-      if (fp == (((uint64_t)slot.w << 32) | slot.z)) {
-        const uint32_t ref = slot.y;
+      const uint32_t ref = slot.y;
+      if (fp == (((uint64_t)slot.w << 32) | slot.z) && cls[ref] == ref) {
         const uint64_t o = anc_off[ref];
         if (pos >= r + o) {
           const uint64_t ws = pos - o, p = ws + W - 1;
@@ -886,10 +921,11 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
   }
 }
 
-__global__ void __launch_bounds__(256) zc_probe_kernel(
+__global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const uint8_t* __restrict__ data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* __restrict__ tab,
     uint32_t tbits, const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off,
-    const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r, uint64_t n, uint32_t W,
+    const uint32_t* __restrict__ cls, const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r,
+    uint64_t n, uint32_t W,
     Cand* __restrict__ cand, uint64_t cand_cap, unsigned long long* __restrict__ counters) {
   const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
@@ -918,14 +954,32 @@ __global__ void __launch_bounds__(256) zc_probe_kernel(
     const uint32_t fb = g[q] & ((1u << kGFiltBits) - 1);
     f[q] = live[q] ? (gfilt[fb >> 5] >> (fb & 31)) & 1u : 0u;
   }
-  // level 3: the rare anchors that pass walk the table
+  // level 3: the offsets of the anchors that pass, compacted into the wave's
+  // LDS list {offset in the wave pair | wave-tile << 24, gear}
+  __shared__ uint2 s_pass[kProbeTPB / 64][kS * 64];
+  uint2* const lst = s_pass[threadIdx.x >> 6];
+  uint32_t rel[kS];
 #pragma unroll
   for (int q = 0; q < kS; ++q) {
-    if (!f[q]) continue;
     const int t = q / kProbeSlots;
-    const uint32_t e = lane + 64u * (q % kProbeSlots);
-    probe_anchor(data, (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e], g[q], tab, tbits, anc_off, vis, dead, r, n, W, cand,
-                 cand_cap, counters);
+    rel[q] = f[q] ? ta[t].rel[lane + 64u * (q % kProbeSlots)] : 0u;
+  }
+  static_assert(ZC_WT_SHIFT < 24 && kProbeWT <= 256, "pass-list packing");
+  uint32_t np = 0;
+#pragma unroll
+  for (int q = 0; q < kS; ++q) {
+    const uint64_t m = __ballot(f[q] != 0u);
+    if (f[q]) lst[np + lane_prefix(m)] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24, g[q]);
+    np += (uint32_t)__popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // level 4: the table walks, one anchor per lane
+  for (uint32_t j = lane; j < np; j += 64) {
+    const uint2 a = lst[j];
+    const uint32_t t = a.x >> 24;
+    probe_anchor(data, ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu), a.y, tab, tbits, anc_off,
+                 cls, vis, dead, r, n, W, cand, cand_cap, counters);
   }
   // wave-tiles with more anchors than the slots above
 #pragma unroll
@@ -934,7 +988,7 @@ __global__ void __launch_bounds__(256) zc_probe_kernel(
       const uint32_t gk = ta[t].g[e];
       const uint32_t fb = gk & ((1u << kGFiltBits) - 1);
       if ((gfilt[fb >> 5] >> (fb & 31)) & 1u)
-        probe_anchor(data, (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e], gk, tab, tbits, anc_off, vis, dead, r, n, W,
+        probe_anchor(data, (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e], gk, tab, tbits, anc_off, cls, vis, dead, r, n, W,
                      cand, cand_cap, counters);
     }
   }
@@ -993,55 +1047,84 @@ __device__ __forceinline__ uint32_t key_slot(uint64_t k, uint32_t bits) {
   return (uint32_t)((k * kGolden) >> (64 - bits));
 }
 
-__global__ void zc_class_insert_kernel(const uint64_t* __restrict__ key, uint32_t nref, uint64_t* ckeys,
-                                       uint32_t* cvals, uint32_t cbits) {
+// thread per ref: the class table (lowest ref per key) and, for a ref with an
+// anchor, the anchor table and its key filter
+__global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off,
+                                       const uint32_t* __restrict__ cg, const uint64_t* __restrict__ cfp,
+                                       uint32_t nref, uint64_t* ckeys, uint32_t* cvals, uint32_t cbits,
+                                       uint64_t* tab, uint32_t tbits, uint32_t* __restrict__ gfilt) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nref) return;
   // a ref with the same key as the ref before it is not the lowest of its
   // key: only the first ref of each run of equal keys inserts (repeated
   // content -- all-zero streams -- would otherwise serialise every ref on
   // one slot's atomics)
-  if (i > 0 && key[i - 1] == key[i]) return;
-  const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
-  const uint32_t mask = (1u << cbits) - 1;
-  for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
-    const unsigned long long prev = atomicCAS((unsigned long long*)&ckeys[h], (unsigned long long)kEmpty,
-                                              (unsigned long long)k);
-    if (prev == kEmpty || prev == k) {
-      atomicMin(&cvals[h], i);
+  if (i == 0 || key[i - 1] != key[i]) {
+    const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
+    const uint32_t mask = (1u << cbits) - 1;
+    for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&ckeys[h], (unsigned long long)kEmpty,
+                                                (unsigned long long)k);
+      if (prev == kEmpty || prev == k) {
+        atomicMin(&cvals[h], i);
+        break;
+      }
+    }
+  }
+  if (!tab || anc_off[i] == ZC_NO_ANCHOR) return;
+  // every ref with an anchor enters the anchor table (the probe keeps class
+  // leaders only: classes are not known yet)
+  const uint32_t g = cg[i];
+  const uint32_t fb = g & ((1u << kGFiltBits) - 1);
+  atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
+  const uint64_t word = ((uint64_t)i << 32) | g;
+  const uint32_t mask = (1u << tbits) - 1;
+  for (uint32_t h = table_slot(g, tbits);; h = (h + 1) & mask) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
+                                              (unsigned long long)word);
+    if (prev == kEmpty) {
+      tab[2 * (uint64_t)h + 1] = cfp[i];
       return;
     }
   }
 }
 
-// one wave per ref: its class = the lowest ref with the same key if the bytes
-// are equal (else itself); counts the refs that are not leaders
-__global__ void __launch_bounds__(256) zc_class_resolve_kernel(const uint8_t* __restrict__ data,
-                                                               const uint64_t* __restrict__ key,
-                                                               const uint64_t* __restrict__ start, uint32_t nref,
-                                                               uint32_t W, const uint64_t* __restrict__ ckeys,
-                                                               const uint32_t* __restrict__ cvals, uint32_t cbits,
-                                                               uint32_t* __restrict__ cls,
-                                                               unsigned long long* __restrict__ counters) {
-  const uint32_t i = (uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+// thread per ref: its class = the lowest ref with the same key if the bytes
+// are equal, else itself (the wave compares the bytes of each of its refs
+// that is not that lowest ref, one range pair at a time); class leaders
+// without an anchor are listed for the exact screen
+__global__ void __launch_bounds__(256) zc_class_resolve_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ key, const uint64_t* __restrict__ start,
+    const uint32_t* __restrict__ anc_off, uint32_t nref, uint32_t W, const uint64_t* __restrict__ ckeys,
+    const uint32_t* __restrict__ cvals, uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
+    unsigned long long* __restrict__ counters) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
-  if (i >= nref) return;
-  const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
-  const uint32_t mask = (1u << cbits) - 1;
-  uint32_t h = key_slot(k, cbits);
-  while (ckeys[h] != k) h = (h + 1) & mask;
-  const uint32_t lead = cvals[h];
-  if (lead == i) {
-    if (lane == 0) cls[i] = i;
-    return;
+  const bool valid = i < nref;
+  uint32_t lead = i;
+  if (valid) {
+    const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
+    const uint32_t mask = (1u << cbits) - 1;
+    uint32_t h = key_slot(k, cbits);
+    while (ckeys[h] != k) h = (h + 1) & mask;
+    lead = cvals[h];
+    cls[i] = i;
+    if (lead == i && anc_off[i] == ZC_NO_ANCHOR) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = i;
   }
-  const bool same = wave_ranges_equal(data, start[i], start[lead], W, lane);
-  if (lane == 0) {
-    cls[i] = same ? lead : i;
-    if (same) atomicAdd(&counters[CNT_CLASS], 1ull);
+  for (uint64_t m = __ballot(valid && lead != i); m; m &= m - 1) {
+    const int l = __builtin_ctzll(m);
+    const uint32_t ri = __shfl(i, l), rl = __shfl(lead, l);
+    const bool same = wave_ranges_equal(data, start[ri], start[rl], W, lane);
+    if (lane == 0) {
+      if (same) {
+        cls[ri] = rl;
+        atomicAdd(&counters[CNT_CLASS], 1ull);
+      } else if (anc_off[ri] == ZC_NO_ANCHOR) {
+        ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = ri;
+      }
+    }
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // zc_range_digest: RollingHash::digest of [a, b) = 257^(b-a) + acc
@@ -1707,66 +1790,41 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
-                             uint32_t nchunks, uint32_t W, uint64_t pw, uint64_t* start, uint64_t* vis,
-                             uint8_t* dead, uint64_t* key, uint32_t* cg, uint64_t* cfp, uint32_t* anc_off,
-                             hipStream_t s) {
-  if (!nchunks) return hipSuccess;
-  hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(nchunks, 128)), dim3(128), 0, s, data, n, blk, av,
-                     r_e, nchunks, W, pw, start, vis, dead, key, cg, cfp, anc_off);
-  return hipGetLastError();
-}
 
-hipError_t launch_anchorless(const uint32_t* anc_off, const uint32_t* cls, uint32_t nref, uint32_t* list,
-                             uint32_t cap, unsigned long long* counters, hipStream_t s) {
-  if (!nref) return hipSuccess;
-  hipLaunchKernelGGL(zc_anchorless_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, anc_off, cls, nref, list,
-                     cap, counters);
-  return hipGetLastError();
-}
 
-hipError_t launch_table_clear(uint64_t* tkeys, uint32_t tsize, hipStream_t s) {
-  hipLaunchKernelGGL(zc_table_clear_kernel, dim3(blocks_for(tsize, 256)), dim3(256), 0, s, tkeys, tsize);
-  return hipGetLastError();
-}
 
-hipError_t launch_table_insert(uint64_t* tab, uint32_t tbits, const uint32_t* cg, const uint64_t* cfp,
-                               const uint32_t* anc_off, const uint32_t* cls, uint32_t nrefs, uint32_t* gfilt,
-                               hipStream_t s) {
-  hipError_t e = hipMemsetAsync(tab, 0xFF, (size_t)16 << tbits, s);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(gfilt, 0, kGFiltWords * sizeof(uint32_t), s);
-  if (e != hipSuccess || !nrefs) return e;
-  hipLaunchKernelGGL(zc_table_insert_kernel, dim3(blocks_for(nrefs, 256)), dim3(256), 0, s, tab, tbits, cg, cfp,
-                     anc_off, cls, nrefs, gfilt);
+
+hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
+                              uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
+                              hipStream_t s) {
+  const uint32_t nref = nconf + nsref;
+  const EpochClear ec{ix.ckeys, ix.cvals, nref ? 1u << ix.cbits : 0u,    ix.tab,
+                      ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters};
+  // enough threads for the grid chunks, and for the clears at a few words each
+  const uint64_t words = (uint64_t)ec.cwords + ec.twords + ec.gwords;
+  const uint64_t threads = std::max<uint64_t>({nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
+  hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
+                     nsref, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf, ix.cg + nconf,
+                     ix.cfp + nconf, ix.anc + nconf, ec);
+  if (!nref) return hipGetLastError();
+  hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
+                     ix.cfp, nref, ix.ckeys, ix.cvals, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
+  hipLaunchKernelGGL(zc_class_resolve_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, data, ix.key, ix.start,
+                     ix.anc, nref, W, ix.ckeys, ix.cvals, ix.cbits, ix.cls, ix.ancless, ix.counters);
   return hipGetLastError();
 }
 
 uint32_t probe_filter_words() { return kGFiltWords; }
 
-hipError_t launch_classes(const uint8_t* data, const uint64_t* key, const uint64_t* start, uint32_t nref, uint32_t W,
-                          uint64_t* ckeys, uint32_t* cvals, uint32_t cbits, uint32_t* cls,
-                          unsigned long long* counters, hipStream_t s) {
-  if (!nref) return hipSuccess;
-  const uint32_t csize = 1u << cbits;
-  hipLaunchKernelGGL(zc_table_clear_kernel, dim3(blocks_for(csize, 256)), dim3(256), 0, s, ckeys, csize);
-  hipError_t e = hipMemsetAsync(cvals, 0xFF, csize * sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(zc_class_insert_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, key, nref, ckeys, cvals,
-                     cbits);
-  hipLaunchKernelGGL(zc_class_resolve_kernel, dim3(blocks_for((uint64_t)nref * 64, 256)), dim3(256), 0, s, data,
-                     key, start, nref, W, ckeys, cvals, cbits, cls, counters);
-  return hipGetLastError();
-}
 
 hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
-                        uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint64_t* vis,
-                        const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand, uint64_t cand_cap,
-                        unsigned long long* counters, hipStream_t s) {
+                        uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint32_t* cls,
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand,
+                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
   const uint64_t waves = (nwt + kProbeWT - 1) / kProbeWT;
-  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(waves * 64, 256)), dim3(256), 0, s, data, av, wt0, nwt, tab,
-                     tbits, gfilt, anc_off, vis, dead, r, p_end, W, cand, cand_cap, counters);
+  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(waves * 64, kProbeTPB)), dim3(kProbeTPB), 0, s, data, av, wt0, nwt, tab,
+                     tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, cand, cand_cap, counters);
   return hipGetLastError();
 }
 
