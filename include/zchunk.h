@@ -79,14 +79,15 @@ typedef struct {
 
 typedef struct {
   double scan_ms;        /* zc_scan kernel (HIP events on the context stream) */
-  double resolve_ms;     /* everything after the scan, wall clock */
+  double resolve_ms;     /* everything after the scan: total_ms - scan_ms with ZC_FLAG_TIMING */
   double total_ms;       /* whole call, wall clock */
   uint64_t bytes;        /* stream length */
   uint64_t anchors;      /* content anchors found by the scan */
   uint64_t candidates;   /* anchor-probe candidates */
   uint64_t epochs;       /* resolution epochs (1 + grid-shifting matches) */
   uint64_t fscan_runs;   /* screen-hit runs from the exact-hash screen */
-  double meta_ms;        /* grid-chunk keys + first anchors (wall clock, summed over epochs) */
+  double meta_ms;        /* epoch index + probe batch (first epoch: device time from the scan's end;
+                            later ones: wall clock; summed) */
   double probe_ms;       /* anchor table + probe + candidate verification */
   double fscan_ms;       /* exact-hash screen */
   double walk_ms;        /* boundary walk + record assembly on the host */

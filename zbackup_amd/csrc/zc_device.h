@@ -187,9 +187,13 @@ hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,
                                uint8_t* ok, hipStream_t s);
 
+// RollingHash digest of each [a[i], b[i]) (device arrays)
 hipError_t launch_range_digest(const uint8_t* data, uint64_t n, const uint64_t* blk,
                                const uint64_t* a, const uint64_t* b, uint32_t nr, uint64_t* out,
                                hipStream_t s);
+// the same for nr <= 4 ranges given by host arrays (passed by value)
+hipError_t launch_range_digest_small(const uint8_t* data, uint64_t n, const uint64_t* blk, const uint64_t* a,
+                                     const uint64_t* b, uint32_t nr, uint64_t* out, hipStream_t s);
 
 // exact screen, lane per 1 KiB: zc_fscan tiles [tile0, tile0 + ntiles) of
 // ZC_TILE bytes, positions p in [p_start, p_end); runs of tile t at

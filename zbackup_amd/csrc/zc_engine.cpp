@@ -162,7 +162,7 @@ struct zc_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_in = nullptr, ev_idx = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   std::string err;
 
   // host feed
@@ -201,6 +201,9 @@ struct zc_ctx {
   DevBuf<Run> runs;
   DevBuf<uint32_t> ancless;
   HostBuf<unsigned long long> h_cnt;
+  HostBuf<unsigned long long> h_scnt;  // the scan's counters, read back with the first epoch's batch
+  HostBuf<uint64_t> h_pre;             // digests of the predicted tail pieces
+  DevBuf<uint64_t> d_pre;
   HostBuf<uint64_t> h_key;  // grid-chunk keys of the current epoch
   HostBuf<uint64_t> h_ra, h_rb, h_rout;  // pinned staging of range-digest batches
 };
@@ -274,10 +277,17 @@ class Resolver {
     hspan_ = 0;
     while (epoch()) {
     }
+    if (!scan_checked_) {  // no epoch synchronised (no refs): for the statistics
+      sync(c_);
+      scan_check();
+    }
     finalize();
     auto t2 = std::chrono::steady_clock::now();
-    c_.stats.resolve_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     c_.stats.total_ms = std::chrono::duration<double, std::milli>(t2 - t_begin_).count();
+    // the resolver's work overlaps the scan's tail (nothing waits for the scan
+    // alone), so the part after the scan is the whole minus the scan
+    c_.stats.resolve_ms = (c_.flags & ZC_FLAG_TIMING) ? std::max(0.0, c_.stats.total_ms - c_.stats.scan_ms)
+                                                      : std::chrono::duration<double, std::milli>(t2 - t1).count();
   }
 
  private:
@@ -400,18 +410,34 @@ class Resolver {
     if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
   }
 
+  // The scan's counters are read back with the first epoch's batch (no
+  // synchronisation between the scan and the epoch): that epoch's device work
+  // is queued assuming no wave-tile overflowed, and redone in the rare case
+  // one did (scan_check).  Overflowed wave-tiles read as empty until then.
   void scan_finish() {
     if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
-    d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
-    sync(c_);
+    c_.h_scnt.ensure(CNT_LAST);
+    d2h(c_, c_.h_scnt.p, c_.counters.p, CNT_LAST);
+    c_.srel.ensure(1);
+    c_.sg.ensure(1);
+    av_ = AnchorView{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p};
+    scan_checked_ = false;
+  }
+
+  // after a synchronisation that covers the scan: anchor count, scan timing,
+  // and the exact rescan of overflowed wave-tiles; true if the anchors changed
+  // (work queued on the provisional pool must be redone)
+  bool scan_check() {
+    if (scan_checked_) return false;
+    scan_checked_ = true;
     if (c_.flags & ZC_FLAG_TIMING) {
       float ms = 0;
       HCK(hipEventElapsedTime(&ms, c_.ev0, c_.ev1));
       c_.stats.scan_ms = ms;
     }
-    npool_ = c_.h_cnt[CNT_POOL];
+    npool_ = c_.h_scnt[CNT_POOL];
     c_.stats.anchors = npool_;
-    if (c_.h_cnt[CNT_OVERFLOW]) {
+    if (c_.h_scnt[CNT_OVERFLOW]) {
       // wave-tiles whose anchors overflowed the scan's LDS list or their pool
       // share (dense data): count them exactly, then rescan into a side pool
       std::vector<uint32_t> cnt(nwt_), tiles, sbase;
@@ -440,18 +466,22 @@ class Resolver {
       h2d(c_, c_.obase.p, sbase.data(), nt);
       HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, c_.obase.p, nt, 1, c_.dbase.p, c_.dcnt.p,
                                c_.srel.p, c_.sg.p, c_.stream));
-    } else {
-      c_.srel.ensure(1);
-      c_.sg.ensure(1);
+      av_ = AnchorView{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p};
+      return true;
     }
-    av_ = AnchorView{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p};
+    return false;
   }
+  bool scan_checked_ = true;
 
   // ---------------------------------------------------------------- epoch
   // One epoch = one grid origin r_e.  Device work is queued back to back
   // (grid-chunk metadata, anchor table, probe, anchorless compaction) and read
   // back with one synchronisation.
   bool epoch() {
+    if (!scan_checked_ && c_.stats.epochs > 0) {
+      sync(c_);
+      scan_check();
+    }
     c_.stats.epochs++;
     r_e_ = s_;
     ks_ = 0;
@@ -503,14 +533,15 @@ class Resolver {
       c_.ckeys.ensure(1u << tbits);
       c_.cvals.ensure(1u << tbits);
       c_.c_cls.ensure(nref_);
-      if (npool_) {
+      const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
+      if (anchors) {
         c_.tab.ensure(2u << tbits);
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         c_.gfilt.ensure(probe_filter_words());
       }
       const EpochIndex ix{c_.c_start.p, c_.c_vis.p,  c_.c_dead.p, c_.c_key.p, c_.c_g.p,
                           c_.c_fp.p,    c_.c_anc.p,  c_.c_cls.p,  c_.ckeys.p, c_.cvals.p,
-                          tbits,        npool_ ? c_.tab.p : nullptr, tbits, c_.gfilt.p, c_.ancless.p,
+                          tbits,        anchors ? c_.tab.p : nullptr, tbits, c_.gfilt.p, c_.ancless.p,
                           c_.counters.p};
       HCK(launch_epoch_index(d_, n_, c_.blk.p, av_, r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
       // the grid chunks' keys go to the host on the side stream while the
@@ -520,12 +551,19 @@ class Resolver {
       if (nsref)
         HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c_.copy_stream));
-      if (npool_)
+      predict_tail();
+      if (anchors)
         HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
                          c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+      const bool first = !scan_checked_;  // this batch also waits for the scan
+      if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
       HCK(hipStreamSynchronize(c_.copy_stream));
+      if (scan_check()) {  // the pool changed under this epoch: queue it again
+        c_.stats.epochs--;
+        return true;
+      }
       ncand = c_.h_cnt[CNT_CAND];
       nancless = c_.h_cnt[CNT_ANCLESS];
       if (c_.h_cnt[CNT_CLASS]) load_classes();
@@ -539,7 +577,13 @@ class Resolver {
         ncand = c_.h_cnt[CNT_CAND];
         if (ncand > c_.cand.cap) throw ZcError{ZC_ERR_NOMEM, "candidate buffer overflow persisted"};
       }
-      c_.stats.meta_ms += ms_since(tm);
+      if (first && (c_.flags & ZC_FLAG_TIMING)) {  // device time from the scan's end
+        float ms = 0;
+        HCK(hipEventElapsedTime(&ms, c_.ev1, c_.ev_meta));
+        c_.stats.meta_ms += ms;
+      } else {
+        c_.stats.meta_ms += ms_since(tm);
+      }
     }
     if (ncand) {
       auto tp = Clock::now();
@@ -567,6 +611,41 @@ class Resolver {
     bool again = walk();
     c_.stats.walk_ms += ms_since(tw);
     return again;
+  }
+
+  // An epoch that reaches the end of the stream ends, if no match comes, with
+  // finish() cutting [s, n) after the last grid chunk s = r_e + nspec W: the
+  // digests of those pieces are computed on the side stream with the epoch's
+  // batch, so the common case needs no round trip in finalize()
+  std::vector<uint64_t> pre_a_, pre_b_;
+  bool pre_ready_ = false;
+  void predict_tail() {
+    pre_a_.clear();
+    pre_b_.clear();
+    pre_ready_ = false;
+    if (h_end_ < n_) return;
+    const uint64_t s = nspec_ ? r_e_ + (uint64_t)nspec_ * W_ : r_e_;
+    if (s >= n_) return;
+    const uint64_t L = n_ - s;
+    auto add = [&](uint64_t a, uint64_t b) {
+      if (b - a >= 128) {
+        pre_a_.push_back(a);
+        pre_b_.push_back(b);
+      }
+    };
+    if (L > W_) {
+      add(s, s + W_);
+      add(s + W_, n_);
+    } else {
+      add(s, n_);
+    }
+    if (pre_a_.empty()) return;
+    const uint32_t nr = (uint32_t)pre_a_.size();
+    c_.d_pre.ensure(nr);
+    c_.h_pre.ensure(nr);
+    HCK(launch_range_digest_small(d_, n_, c_.blk.p, pre_a_.data(), pre_b_.data(), nr, c_.d_pre.p, c_.copy_stream));
+    HCK(hipMemcpyAsync(c_.h_pre.p, c_.d_pre.p, nr * sizeof(uint64_t), hipMemcpyDeviceToHost, c_.copy_stream));
+    pre_ready_ = true;  // read after the epoch's copy-stream synchronisation
   }
 
   // wave-tiles holding the anchors of windows ending in [x0, h_end)
@@ -1125,12 +1204,21 @@ class Resolver {
       ~Done() { st.finalize_ms += ms_since(t); }
     } done{c_.stats, t0};
     std::vector<uint64_t> a, b;
-    for (auto& pc : need_digest_) {
-      a.push_back(pc.a);
-      b.push_back(pc.b);
+    std::vector<size_t> rest;
+    for (size_t i = 0; i < need_digest_.size(); ++i) {
+      const Piece& pc = need_digest_[i];
+      size_t k = 0;
+      while (pre_ready_ && k < pre_a_.size() && !(pre_a_[k] == pc.a && pre_b_[k] == pc.b)) ++k;
+      if (pre_ready_ && k < pre_a_.size()) {
+        c_.recs[pc.rec].rolling = c_.h_pre[k];
+      } else {
+        a.push_back(pc.a);
+        b.push_back(pc.b);
+        rest.push_back(i);
+      }
     }
     std::vector<uint64_t> h = range_digests(a, b);
-    for (size_t i = 0; i < need_digest_.size(); ++i) c_.recs[need_digest_[i].rec].rolling = h[i];
+    for (size_t j = 0; j < rest.size(); ++j) c_.recs[need_digest_[rest[j]].rec].rolling = h[j];
     if (c_.flags & ZC_FLAG_SHA1) {
       std::vector<uint64_t> sa;
       std::vector<uint32_t> sl;
@@ -1221,6 +1309,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     HCK(hipEventCreate(&c->ev0));
     HCK(hipEventCreate(&c->ev1));
+    HCK(hipEventCreate(&c->ev_meta));
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
@@ -1243,6 +1332,7 @@ int zc_destroy(zc_ctx* c) {
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_meta) (void)hipEventDestroy(c->ev_meta);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);

@@ -778,7 +778,8 @@ struct TileAnchors {
 };
 
 __device__ __forceinline__ TileAnchors tile_anchors(const AnchorView& av, uint64_t wt) {
-  const uint32_t b = av.base[wt], c = av.cnt[wt];
+  // a wave-tile still marked overflowed (before its exact rescan) reads empty
+  const uint32_t b = av.base[wt], c0 = av.cnt[wt], c = c0 == ZC_WT_OVERFLOW ? 0u : c0;
   if (b & ZC_SIDE_POOL) return TileAnchors{av.srel + (b & ~ZC_SIDE_POOL), av.sg + (b & ~ZC_SIDE_POOL), c};
   return TileAnchors{av.rel + b, av.g + b, c};
 }
@@ -1135,6 +1136,19 @@ __global__ void zc_range_digest_kernel(const uint8_t* __restrict__ data, uint64_
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nr) return;
   out[i] = pow257_dev(b[i] - a[i]) + rk_acc(data, blk, a[i], b[i]);
+}
+
+// the same for at most kSmallRanges ranges passed by value (no upload)
+constexpr uint32_t kSmallRanges = 4;
+struct SmallRanges {
+  uint64_t a[kSmallRanges], b[kSmallRanges];
+  uint32_t nr;
+};
+__global__ void zc_range_digest_small_kernel(const uint8_t* __restrict__ data, uint64_t n,
+                                             const uint64_t* __restrict__ blk, SmallRanges rg,
+                                             uint64_t* __restrict__ out) {
+  const uint32_t i = threadIdx.x;
+  if (i < rg.nr) out[i] = pow257_dev(rg.b[i] - rg.a[i]) + rk_acc(data, blk, rg.a[i], rg.b[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1833,6 +1847,20 @@ hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start, c
   if (!npairs) return hipSuccess;
   hipLaunchKernelGGL(zc_verify_kernel, dim3(blocks_for((uint64_t)npairs * 64, 256)), dim3(256), 0, s,
                      data, win_start, ref_start, len, npairs, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_range_digest_small(const uint8_t* data, uint64_t n, const uint64_t* blk, const uint64_t* a,
+                                     const uint64_t* b, uint32_t nr, uint64_t* out, hipStream_t s) {
+  if (!nr) return hipSuccess;
+  if (nr > kSmallRanges) return hipErrorInvalidValue;
+  SmallRanges rg{};
+  for (uint32_t k = 0; k < nr; ++k) {
+    rg.a[k] = a[k];
+    rg.b[k] = b[k];
+  }
+  rg.nr = nr;
+  hipLaunchKernelGGL(zc_range_digest_small_kernel, dim3(1), dim3(64), 0, s, data, n, blk, rg, out);
   return hipGetLastError();
 }
 
