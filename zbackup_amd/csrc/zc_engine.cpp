@@ -31,11 +31,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <iterator>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -153,8 +158,85 @@ struct DefaultInit : std::allocator<T> {
   }
 };
 
-}  // namespace
+// A few host threads for the record writing of long grid runs (a stream's
+// records are ~40 bytes each, 131,072 per 8 GiB: one core writes them at its
+// store bandwidth).  Workers sleep between jobs; the caller takes a share.
+class HostPool {
+ public:
+  static HostPool& get() {
+    // one pool per process: a forked child gets its own (the parent's
+    // workers do not exist there); the old one is left as it is
+    static std::mutex mk;
+    static HostPool* pool = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> lk(mk);
+    if (!pool || owner != getpid()) {
+      pool = new HostPool;
+      owner = getpid();
+    }
+    return *pool;
+  }
+  // f(begin, end) over [0, n) in kParts contiguous parts
+  void run(size_t n, const std::function<void(size_t, size_t)>& f) {
+    std::lock_guard<std::mutex> one(run_);  // one job at a time (contexts may share the pool)
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &f;
+      n_ = n;
+      pending_ = kWorkers;
+      ++gen_;
+    }
+    cv_.notify_all();
+    part(0, n, f);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
 
+ private:
+  static constexpr int kWorkers = 3, kParts = kWorkers + 1;
+  HostPool() {
+    for (int w = 0; w < kWorkers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
+  }
+  static void part(int k, size_t n, const std::function<void(size_t, size_t)>& f) {
+    const size_t a = n * k / kParts, b = n * (k + 1) / kParts;
+    if (b > a) f(a, b);
+  }
+  void loop(int k) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(m_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (stop_) return;
+      const auto* f = job_;
+      const size_t n = n_;
+      lk.unlock();
+      part(k, n, *f);
+      lk.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex run_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(size_t, size_t)>* job_ = nullptr;
+  size_t n_ = 0;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+}  // namespace
 
 struct zc_ctx {
   int device = 0;
@@ -321,6 +403,8 @@ class Resolver {
   std::vector<uint64_t> cstart_, ckey_, cfp_;  // cfp_: 64-byte anchor fingerprint
   std::vector<uint32_t> canc_, cg_;            // cg_: anchor gear value
   std::vector<uint8_t> dead_;
+  uint64_t ndead_ = 0;  // refs of this epoch consumed by same-grid matches
+  static constexpr uint64_t kParallelRecords = 32768;
   uint32_t nconf_ = 0, nspec_ = 0, nref_ = 0;
   uint64_t ks_ = 0;  // next grid chunk of this epoch to save
 
@@ -497,6 +581,7 @@ class Resolver {
     const uint32_t nsref = indexable_ ? nspec_ : 0;
     nref_ = nconf_ + nsref;
     dead_.assign(nref_, 0);
+    ndead_ = 0;
     cls_.clear();
     acands_.clear();
     runs_.clear();
@@ -1072,6 +1157,27 @@ class Resolver {
     zc_record* rec = c_.recs.data();
     const uint32_t kind = indexable_ ? (uint32_t)ZC_CHUNK_NEW : (uint32_t)ZC_BYTES;
     const uint8_t* dead = indexable_ ? dead_.data() + nconf_ : nullptr;
+    if (ndead_ == 0 && r_e_ + ks_ * W_ >= s_ && kmax - ks_ >= kParallelRecords) {
+      // every chunk of the run is saved: record o + j is grid chunk ks_ + j
+      const uint64_t k0 = ks_, r0 = r_e_;
+      const uint32_t W = W_;
+      const bool idx = indexable_;
+      const uint64_t* key = c_.h_key.p;
+      zc_record* out = rec + o;
+      HostPool::get().run(kmax - ks_, [&](size_t a, size_t b) {
+        for (size_t j = a; j < b; ++j) {
+          zc_record& r = out[j];
+          r.offset = r0 + (k0 + j) * W;
+          r.size = W;
+          r.kind = kind;
+          r.rolling = idx ? key[k0 + j] : 0;
+          memset(r.sha1, 0, sizeof r.sha1);
+        }
+      });
+      s_ = r_e_ + kmax * W_;
+      ks_ = kmax;
+      return;
+    }
     for (uint64_t k = ks_; k < kmax; ++k) {
       const uint64_t ck = r_e_ + k * W_;
       if ((dead && dead[k]) || ck < s_) continue;
@@ -1155,7 +1261,10 @@ class Resolver {
       if ((r_ - r_e_) % W_ == 0) {
         // same grid: the grid chunk the window covered is consumed, not saved
         const uint64_t j = (ws - r_e_) / W_;
-        if (indexable_ && j < nspec_) dead_[nconf_ + j] = 1;
+        if (indexable_ && j < nspec_) {
+          dead_[nconf_ + j] = 1;
+          ++ndead_;
+        }
         if (j >= ks_) ks_ = j + 1;
         x = r_ + W_ - 1;
         continue;
