@@ -147,6 +147,9 @@ int main() {
 #define STR(ROT) vs.push_back({"stage tpb=512 rowb=128 slots=2 stride=4096 rot=" #ROT, [=] { \
     uint64_t nt = n / (512 * 4096ull); hipLaunchKernelGGL((stage_kernel<512, 128, 2, 0, false, 4096, ROT>), dim3(std::min<uint64_t>(nt, (uint64_t)cus)), dim3(512), 0, 0, d, nt, out); }, {}});
   STR(2) STR(4) STR(8) STR(32)
+#define STV(ROWB, SLOTS, EXTRA) vs.push_back({"stage rot=2 rowb=" #ROWB " slots=" #SLOTS " extra=" #EXTRA, [=] { \
+    uint64_t nt = n / (512 * 4096ull); hipLaunchKernelGGL((stage_kernel<512, ROWB, SLOTS, EXTRA, false, 4096, 2>), dim3(std::min<uint64_t>(nt, (uint64_t)cus)), dim3(512), 0, 0, d, nt, out); }, {}});
+  STV(128, 2, 0) STV(128, 2, 8) STV(128, 2, 10) STV(64, 4, 0) STV(64, 4, 8) STV(64, 4, 10) STV(64, 3, 8) STV(256, 1, 8)
 #define REG(TPB, DEPTH, EXTRA, WPC) vs.push_back({"reg tpb=" #TPB " depth=" #DEPTH " extra=" #EXTRA " wg/cu=" #WPC, [=] { \
     hipLaunchKernelGGL((reg_kernel<TPB, DEPTH, EXTRA>), dim3(cus * WPC), dim3(TPB), 0, 0, d, n / 8192, out); }, {}});
   REG(512, 2, 0, 1)
