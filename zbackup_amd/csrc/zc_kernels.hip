@@ -88,14 +88,22 @@ __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __r
   const uint64_t m = span_mul();
   uint64_t k = a_up / ZC_SPAN;
   const uint64_t k1 = b_dn / ZC_SPAN;
-  // span digests eight loads at a time (the fold is a dependent chain; the
+  // span digests sixteen loads at a time (the fold is a dependent chain; the
   // loads need not be)
-  for (; k + 8 <= k1; k += 8) {
+  for (; k + 16 <= k1; k += 16) {
+    uint64_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = blk[k + i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = acc * m + v[i];
+  }
+  if (k + 8 <= k1) {
     uint64_t v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = blk[k + i];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc = acc * m + v[i];
+    k += 8;
   }
   for (; k < k1; ++k) acc = acc * m + blk[k];
   for (uint64_t i = b_dn; i < b; ++i) acc = acc * 257u + data[i];
@@ -832,10 +840,29 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
       const TileAnchors ta = tile_anchors(av, wt);
       const uint64_t t0 = wt << ZC_WT_SHIFT;
       const uint32_t lo_rel = lo > t0 ? (uint32_t)(lo - t0) : 0u;
-      uint32_t L = 0, R = ta.cnt;  // first entry with rel >= lo_rel
-      while (L < R) {
-        const uint32_t mid = (L + R) >> 1;
-        if (ta.rel[mid] < lo_rel) L = mid + 1; else R = mid;
+      // first entry with rel >= lo_rel: it lies in [L, R] (R = cnt: none);
+      // a 4-way search loads three pivots per step (a quarter of the
+      // dependent loads of a binary search), then the last <= 3 at once
+      uint32_t L = 0, R = ta.cnt;
+      while (R - L > 3) {
+        const uint32_t q = (R - L) >> 2, a = L + q, b = L + 2 * q, c = L + 3 * q;
+        const uint32_t ra = ta.rel[a], rb = ta.rel[b], rc = ta.rel[c];
+        if (rc < lo_rel) {
+          L = c + 1;
+        } else if (rb < lo_rel) {
+          L = b + 1;
+          R = c;
+        } else if (ra < lo_rel) {
+          L = a + 1;
+          R = b;
+        } else {
+          R = a;
+        }
+      }
+      {
+        const bool b0 = L < R && ta.rel[L] < lo_rel, b1 = L + 1 < R && ta.rel[L + 1] < lo_rel,
+                   b2 = L + 2 < R && ta.rel[L + 2] < lo_rel;
+        L += (uint32_t)b0 + (uint32_t)b1 + (uint32_t)b2;  // sorted: a prefix is below
       }
       if (L < ta.cnt) {
         const uint64_t pos = t0 + ta.rel[L];
@@ -1054,13 +1081,18 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
                                        const uint32_t* __restrict__ cg, const uint64_t* __restrict__ cfp,
                                        uint32_t nref, uint64_t* ckeys, uint32_t* cvals, uint32_t cbits,
                                        uint64_t* tab, uint32_t tbits, uint32_t* __restrict__ gfilt) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nref) return;
+  // threads [0, nref) insert into the class table, [nref, 2 nref) into the
+  // anchor table: the two CAS chains run side by side
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * nref) return;
+  const bool cls_part = t < nref;
+  const uint32_t i = cls_part ? t : t - nref;
   // a ref with the same key as the ref before it is not the lowest of its
   // key: only the first ref of each run of equal keys inserts (repeated
   // content -- all-zero streams -- would otherwise serialise every ref on
   // one slot's atomics)
-  if (i == 0 || key[i - 1] != key[i]) {
+  if (cls_part) {
+    if (i > 0 && key[i - 1] == key[i]) return;
     const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
     const uint32_t mask = (1u << cbits) - 1;
     for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
@@ -1068,7 +1100,7 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
                                                 (unsigned long long)k);
       if (prev == kEmpty || prev == k) {
         atomicMin(&cvals[h], i);
-        break;
+        return;
       }
     }
   }
@@ -1821,7 +1853,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                      nsref, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf, ix.cg + nconf,
                      ix.cfp + nconf, ix.anc + nconf, ec);
   if (!nref) return hipGetLastError();
-  hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
+  hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
                      ix.cfp, nref, ix.ckeys, ix.cvals, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
   hipLaunchKernelGGL(zc_class_resolve_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, data, ix.key, ix.start,
                      ix.anc, nref, W, ix.ckeys, ix.cvals, ix.cbits, ix.cls, ix.ancless, ix.counters);
