@@ -708,20 +708,26 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
           for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
     }
-    v4u32 vr[kPieces];
+    static_assert(kPieces == 8, "the round is read in two halves of four pieces");
+    v4u32 va[4], vb[4];
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) vr[p] = lds_read16(row + lane * ZC_ROUND + ((p ^ sw) << 4));
+    for (int p = 0; p < 4; ++p) va[p] = lds_read16(row + lane * ZC_ROUND + ((p ^ sw) << 4));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) vb[p] = lds_read16(row + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
+    // the first four pieces are hashed while the last four are still in flight
+    wait_lgkmcnt<4>();
+    ties(va);
+    const bool tile_end = r == kRounds - 1 && !(ABL & ABL_NO_TILE_END);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) scan_piece<ABL>(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
     wait_lgkmcnt<0>();  // the slot is free
-    ties(vr);
-    uint4 v[kPieces];
-#pragma unroll
-    for (int p = 0; p < kPieces; ++p) v[p] = to_uint4(vr[p]);
+    ties(vb);
     // a tile's last round issues the DMA two ahead only after the tile end,
     // which uses the slot just read to stage the anchors
-    const bool tile_end = r == kRounds - 1 && !(ABL & ABL_NO_TILE_END);
     if (R + 2 < nR && !tile_end) issue(R + 2);
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) scan_piece<ABL>(v[p], pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
+    for (int p = 0; p < 4; ++p)
+      scan_piece<ABL>(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const uint32_t q = pr / (ZC_SPAN / ZC_ROUND);  // per lane: the halves are rotated
