@@ -92,8 +92,18 @@ __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __r
   // loads need not be)
   for (; k + 16 <= k1; k += 16) {
     uint64_t v[16];
+    if ((k & 1) == 0) {  // 16-byte loads, two digests each
+      const uint4* q = (const uint4*)(blk + k);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = blk[k + i];
+      for (int i = 0; i < 8; ++i) {
+        const uint4 t = q[i];
+        v[2 * i] = ((uint64_t)t.y << 32) | t.x;
+        v[2 * i + 1] = ((uint64_t)t.w << 32) | t.z;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = blk[k + i];
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc = acc * m + v[i];
   }
@@ -906,7 +916,7 @@ constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
 // confirmed by the 64-byte fingerprint).  A wave takes kProbeWT consecutive
 // wave-tiles and a lane their slots lane, lane + 64, ... (kProbeSlots per
 // wave-tile; slots past that -- dense small-W streams, side-pool wave-tiles --
-// in a second loop).
+// in a second loop; the geometry is chosen at the launch).
 // The loads are issued level by level -- every slot's gear value, then every
 // filter word -- so a lane has all of them in flight at once; an anchor
 // tests the table's 2^20-bit key filter (L2 resident, ~1 in 8 pass at
@@ -914,8 +924,6 @@ constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
 // wave are compacted into LDS and walked one per lane, so the table walks
 // (a few dependent loads each) run side by side instead of one slot after
 // another.
-constexpr int kProbeWT = 2;     // wave-tiles per wave
-constexpr int kProbeSlots = 4;  // slots per lane per wave-tile (covers wcap <= 256)
 constexpr int kProbeTPB = 256;
 
 __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
@@ -955,6 +963,7 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
   }
 }
 
+template <int kProbeWT, int kProbeSlots>
 __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const uint8_t* __restrict__ data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* __restrict__ tab,
     uint32_t tbits, const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off,
@@ -1874,9 +1883,15 @@ hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64
                         const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand,
                         uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
-  const uint64_t waves = (nwt + kProbeWT - 1) / kProbeWT;
-  hipLaunchKernelGGL(zc_probe_kernel, dim3(blocks_for(waves * 64, kProbeTPB)), dim3(kProbeTPB), 0, s, data, av, wt0, nwt, tab,
-                     tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, cand, cand_cap, counters);
+  // 4 wave-tiles per wave, 2 slots per lane each (128 anchors per wave-tile
+  // before the extra loop; 64 expected at W = 64 KiB): 60 us per 8 GiB vs 68
+  // for 2 x 4 and 8 x 2 (the probe is bound by its random reads: ~100 MB of
+  // table slots and fingerprint bytes per 8 GiB)
+  constexpr int kWT = 4, kSlots = 2;
+  const uint64_t waves = (nwt + kWT - 1) / kWT;
+  hipLaunchKernelGGL((zc_probe_kernel<kWT, kSlots>), dim3(blocks_for(waves * 64, kProbeTPB)), dim3(kProbeTPB), 0, s,
+                     data, av, wt0, nwt, tab, tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, cand, cand_cap,
+                     counters);
   return hipGetLastError();
 }
 
