@@ -137,7 +137,7 @@ def main():
     scan_ms = []
     for _ in range(args.steps):
         bc.chunk_device(buf.data_ptr(), n)
-        scan_ms.append(bc.stats()["scan_ms"])
+        scan_ms.append(bc.scan_ms())
     barrier()
     elapsed = time.perf_counter() - t0
     st = bc.stats()

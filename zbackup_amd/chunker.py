@@ -152,6 +152,15 @@ class BackupCreator:
         _check(self._L, self._ctx, self._L.zc_get_stats(self._ctx, ctypes.byref(st)), "zc_get_stats")
         return {name: getattr(st, name) for name, _ in _lib.ZcStats._fields_}
 
+    def scan_ms(self):
+        """zc_stats.scan_ms of the last stream, without building the stats dict
+        (bench.py reads it inside its timed loop)."""
+        st = getattr(self, "_st_buf", None)
+        if st is None:
+            st = self._st_buf = _lib.ZcStats()
+        _check(self._L, self._ctx, self._L.zc_get_stats(self._ctx, ctypes.byref(st)), "zc_get_stats")
+        return st.scan_ms
+
     def reset(self):
         _check(self._L, self._ctx, self._L.zc_reset(self._ctx), "zc_reset")
         self._data_taken = False

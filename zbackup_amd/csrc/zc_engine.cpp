@@ -203,7 +203,7 @@ class HostPool {
   }
 
  private:
-  static constexpr int kWorkers = 3, kParts = kWorkers + 1;
+  static constexpr int kWorkers = 7, kParts = kWorkers + 1;
   HostPool() {
     for (int w = 0; w < kWorkers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
   }
@@ -630,16 +630,17 @@ class Resolver {
                           c_.counters.p};
       HCK(launch_epoch_index(d_, n_, c_.blk.p, av_, r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
       // the grid chunks' keys go to the host on the side stream while the
-      // probe runs
+      // probe runs (the probe is queued first: nothing waits for the host to
+      // set up the side stream)
       HCK(hipEventRecord(c_.ev_idx, c_.stream));
+      if (anchors)
+        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
       if (nsref)
         HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c_.copy_stream));
       predict_tail();
-      if (anchors)
-        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
-                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
       const bool first = !scan_checked_;  // this batch also waits for the scan
       if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
