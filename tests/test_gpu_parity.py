@@ -118,6 +118,19 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
+# long runs of grid chunks (>= 32,768 records at once) are written by the host
+# thread pool; the runs here are cut by a same-grid match (dead refs: the
+# serial path) and by a grid-shifting one (a new epoch's run)
+@pytest.mark.parametrize("spec", ["R3:6000000", "R3:6000000,C1000:5120,R4:6000000",
+                                  "R3:4194304,C4194300:6000,R4:4500000"])
+def test_long_grid_runs_vs_oracle(torch_cuda, spec):
+    W = 128
+    data = oracle.gen(spec)
+    want = oracle.chunk(data, W)
+    assert sum(1 for r in want if r[0] == "N") >= 32768
+    assert _run_device(torch_cuda, data, W) == want
+
+
 def _dense_anchor_pattern(W, period=16):
     """A `period`-byte pattern whose periodic extension has an anchor in every
     period at chunk size W (the gear of zc_device.h: sum b[q-j] 2^j mod 2^32 >=
