@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host(pinned)->HBM + chunking")
+    ap.add_argument("--sha1", action="store_true",
+                    help="records carry SHA-1 chunk ids (ZC_FLAG_SHA1; the full chunk_to_emit content)")
     return ap.parse_args()
 
 
@@ -123,19 +125,26 @@ def main():
         fill_splitmix64(buf.data_ptr(), n, seed, local)
     torch.cuda.synchronize()
 
-    bc = BackupCreator(W64, device=local, sha1=False, timing=True)
+    # with --sha1 a context's chunks join its index (Writer::add ->
+    # ChunkIndex::addChunk), so chunking the same stream again would measure
+    # an incremental backup of identical data: every step gets a fresh
+    # context there (created before the timed region)
+    ctxs = [BackupCreator(W64, device=local, sha1=args.sha1, timing=True)
+            for _ in range(args.warmup + args.steps if args.sha1 else 1)]
+    bc = ctxs[0]
 
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        bc.chunk_device(buf.data_ptr(), n)
+    for k in range(args.warmup):
+        ctxs[k % len(ctxs)].chunk_device(buf.data_ptr(), n)
     barrier()
     t0 = time.perf_counter()
     scan_ms = []
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        bc = ctxs[(args.warmup + k) % len(ctxs)]
         bc.chunk_device(buf.data_ptr(), n)
         scan_ms.append(bc.scan_ms())
     barrier()
@@ -189,7 +198,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64-seeded bytes generated in HBM)",
             "config": {"workload": CONFIGS[args.config], "stream_bytes_per_gpu": n,
-                       "chunk_max_size": W64, "parallelism": f"replicas x{world} (independent streams)"},
+                       "chunk_max_size": W64, "parallelism": f"replicas x{world} (independent streams)",
+                       "chunk_ids": "SHA-1 prefix + rolling hash" if args.sha1 else "rolling hash"},
             "chunks_per_s": round(nrec * world * args.steps / elapsed, 1),
             "records_per_stream": nrec,
             "roofline": {"bound": "hbm", "kernel": "zc_scan_kernel", "achieved": round(achieved, 1),
@@ -208,7 +218,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_mib << 20, seed)
         print(json.dumps(out), flush=True)
-    bc.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

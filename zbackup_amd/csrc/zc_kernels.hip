@@ -1741,10 +1741,36 @@ __global__ void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t*
   const uint32_t L = len[i];
   uint32_t w[16];
   uint32_t full = L / 64;
-  for (uint32_t blkI = 0; blkI < full; ++blkI) {
+  if ((base & 15) == 0) {
+    // aligned ranges (every grid chunk): 16-byte loads, the next block's
+    // loads in flight while the current one is hashed
+    const uint4* p = (const uint4*)(data + base);
+    uint4 nx[4] = {};
+    if (full) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = bswap32(load4_any(data, base + (uint64_t)blkI * 64 + 4 * k));
-    sha1_block(st, w);
+      for (int k = 0; k < 4; ++k) nx[k] = p[k];
+    }
+    for (uint32_t blkI = 0; blkI < full; ++blkI) {
+      const uint4 cur[4] = {nx[0], nx[1], nx[2], nx[3]};
+      if (blkI + 1 < full) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nx[k] = p[4 * (blkI + 1) + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        w[4 * k] = bswap32(cur[k].x);
+        w[4 * k + 1] = bswap32(cur[k].y);
+        w[4 * k + 2] = bswap32(cur[k].z);
+        w[4 * k + 3] = bswap32(cur[k].w);
+      }
+      sha1_block(st, w);
+    }
+  } else {
+    for (uint32_t blkI = 0; blkI < full; ++blkI) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap32(load4_any(data, base + (uint64_t)blkI * 64 + 4 * k));
+      sha1_block(st, w);
+    }
   }
   // final block(s): remaining bytes, 0x80, zeros, 64-bit big-endian bit length
   uint32_t rem = L - full * 64;
