@@ -161,8 +161,7 @@ struct EpochIndex {
   uint64_t* cfp;
   uint32_t* anc;
   uint32_t* cls;
-  uint64_t* ckeys;
-  uint32_t* cvals;
+  uint64_t* ckeys;  // class table: 2^cbits slots {key high word | lowest ref}
   uint32_t cbits;
   uint64_t* tab;
   uint32_t tbits;

@@ -270,7 +270,7 @@ struct zc_ctx {
   DevBuf<uint32_t> c_anc, c_g;
   DevBuf<uint8_t> c_dead;
   DevBuf<uint64_t> ckeys;
-  DevBuf<uint32_t> cvals, c_cls;
+  DevBuf<uint32_t> c_cls;
   DevBuf<uint64_t> tab;     // anchor table: 16-byte slots {gear | ref << 32, fingerprint}
   DevBuf<uint32_t> gfilt;   // its key filter
   DevBuf<Cand> cand;
@@ -616,7 +616,6 @@ class Resolver {
       while ((1u << tbits) < 2u * nref_) ++tbits;
       // content classes: identical refs share one leader in the table
       c_.ckeys.ensure(1u << tbits);
-      c_.cvals.ensure(1u << tbits);
       c_.c_cls.ensure(nref_);
       const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
       if (anchors) {
@@ -624,10 +623,10 @@ class Resolver {
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         c_.gfilt.ensure(probe_filter_words());
       }
-      const EpochIndex ix{c_.c_start.p, c_.c_vis.p,  c_.c_dead.p, c_.c_key.p, c_.c_g.p,
-                          c_.c_fp.p,    c_.c_anc.p,  c_.c_cls.p,  c_.ckeys.p, c_.cvals.p,
-                          tbits,        anchors ? c_.tab.p : nullptr, tbits, c_.gfilt.p, c_.ancless.p,
-                          c_.counters.p};
+      const EpochIndex ix{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
+                          c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
+                          c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
+                          c_.gfilt.p,   c_.ancless.p, c_.counters.p};
       HCK(launch_epoch_index(d_, n_, c_.blk.p, av_, r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
       // the grid chunks' keys go to the host on the side stream while the
       // probe runs (the probe is queued first: nothing waits for the host to

@@ -811,8 +811,7 @@ __device__ __forceinline__ TileAnchors tile_anchors(const AnchorView& av, uint64
 // ---------------------------------------------------------------------------
 // the epoch's tables and counters, cleared by the chunk-metadata launch
 struct EpochClear {
-  uint64_t* ckeys;  // class table keys: empty
-  uint32_t* cvals;  // class table leaders: none
+  uint64_t* ckeys;  // class table {key high word | lowest ref}: empty
   uint32_t cwords;
   uint64_t* tab;  // anchor table: empty (null: none)
   uint64_t twords;
@@ -833,10 +832,7 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
                                      uint32_t* __restrict__ anc_off, EpochClear ec) {
   const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = gt; j < ec.cwords; j += gs) {
-    ec.ckeys[j] = ~0ull;
-    ec.cvals[j] = ~0u;
-  }
+  for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
   if (ec.tab)
     for (uint64_t j = gt; j < ec.twords; j += gs) ec.tab[j] = ~0ull;
   for (uint64_t j = gt; j < ec.gwords; j += gs) ec.gfilt[j] = 0u;
@@ -1094,7 +1090,7 @@ __device__ __forceinline__ uint32_t key_slot(uint64_t k, uint32_t bits) {
 // anchor, the anchor table and its key filter
 __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off,
                                        const uint32_t* __restrict__ cg, const uint64_t* __restrict__ cfp,
-                                       uint32_t nref, uint64_t* ckeys, uint32_t* cvals, uint32_t cbits,
+                                       uint32_t nref, uint64_t* ckeys, uint32_t cbits,
                                        uint64_t* tab, uint32_t tbits, uint32_t* __restrict__ gfilt) {
   // threads [0, nref) insert into the class table, [nref, 2 nref) into the
   // anchor table: the two CAS chains run side by side
@@ -1107,14 +1103,19 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
   // content -- all-zero streams -- would otherwise serialise every ref on
   // one slot's atomics)
   if (cls_part) {
+    // a slot is {high word of the key | lowest ref}: one CAS inserts a new
+    // key; a ref of a key already present lowers the slot's ref with a
+    // 64-bit atomicMin (equal high words: the minimum is the lower ref)
     if (i > 0 && key[i - 1] == key[i]) return;
-    const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
+    const uint64_t k = key[i];
+    const uint64_t word = (k & 0xFFFFFFFF00000000ull) | i;  // != kEmpty: i < 2^32 - 1
     const uint32_t mask = (1u << cbits) - 1;
     for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
       const unsigned long long prev = atomicCAS((unsigned long long*)&ckeys[h], (unsigned long long)kEmpty,
-                                                (unsigned long long)k);
-      if (prev == kEmpty || prev == k) {
-        atomicMin(&cvals[h], i);
+                                                (unsigned long long)word);
+      if (prev == kEmpty) return;
+      if ((prev >> 32) == (k >> 32) && key[(uint32_t)prev] == k) {
+        atomicMin((unsigned long long*)&ckeys[h], (unsigned long long)word);
         return;
       }
     }
@@ -1144,18 +1145,22 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
 __global__ void __launch_bounds__(256) zc_class_resolve_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ key, const uint64_t* __restrict__ start,
     const uint32_t* __restrict__ anc_off, uint32_t nref, uint32_t W, const uint64_t* __restrict__ ckeys,
-    const uint32_t* __restrict__ cvals, uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
+    uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
     unsigned long long* __restrict__ counters) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
   const bool valid = i < nref;
   uint32_t lead = i;
   if (valid) {
-    const uint64_t k = key[i] == kEmpty ? kEmpty - 1 : key[i];
+    const uint64_t k = key[i];
     const uint32_t mask = (1u << cbits) - 1;
     uint32_t h = key_slot(k, cbits);
-    while (ckeys[h] != k) h = (h + 1) & mask;
-    lead = cvals[h];
+    uint64_t w;
+    for (;; h = (h + 1) & mask) {  // the key's slot: equal high word and an equal key at its ref
+      w = ckeys[h];
+      if ((w >> 32) == (k >> 32) && key[(uint32_t)w] == k) break;
+    }
+    lead = (uint32_t)w;
     cls[i] = i;
     if (lead == i && anc_off[i] == ZC_NO_ANCHOR) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = i;
   }
@@ -1885,7 +1890,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
                               hipStream_t s) {
   const uint32_t nref = nconf + nsref;
-  const EpochClear ec{ix.ckeys, ix.cvals, nref ? 1u << ix.cbits : 0u,    ix.tab,
+  const EpochClear ec{ix.ckeys, nref ? 1u << ix.cbits : 0u, ix.tab,
                       ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters};
   // enough threads for the grid chunks, and for the clears at a few words each
   const uint64_t words = (uint64_t)ec.cwords + ec.twords + ec.gwords;
@@ -1895,9 +1900,9 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                      ix.cfp + nconf, ix.anc + nconf, ec);
   if (!nref) return hipGetLastError();
   hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
-                     ix.cfp, nref, ix.ckeys, ix.cvals, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
+                     ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
   hipLaunchKernelGGL(zc_class_resolve_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, data, ix.key, ix.start,
-                     ix.anc, nref, W, ix.ckeys, ix.cvals, ix.cbits, ix.cls, ix.ancless, ix.counters);
+                     ix.anc, nref, W, ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.counters);
   return hipGetLastError();
 }
 
