@@ -39,6 +39,8 @@ int main(int argc, char** argv) {
     {"gear_nobranch", zc_scan_kernel<ABL_NO_BRANCH | ABL_NO_DIGEST>, {}},
     {"full_never_taken", zc_scan_kernel<ABL_NEVER>, {}},
     {"gear_never_taken", zc_scan_kernel<ABL_NEVER | ABL_NO_DIGEST>, {}},
+    {"te_digest_only", zc_scan_kernel<ABL_TE_DIGEST_ONLY>, {}},
+    {"stage_only_te_digest", zc_scan_kernel<ABL_NO_BYTES | ABL_TE_DIGEST_ONLY>, {}},
   };
   for (int round = 0; round < 12; ++round)
     for (auto& v : vs) {

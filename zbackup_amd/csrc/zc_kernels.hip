@@ -200,9 +200,10 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 // 8 = skip the per-byte work entirely (staging + reads only),
 // 16 = gear + max computed but folded into the state without a ballot/branch,
 // 32 = anchor threshold raised so the recording block is (almost) never taken,
-// 64 = no tile-end work (span digests, anchors to the pool)
+// 64 = no tile-end work (span digests, anchors to the pool), 128 = no
+// counter atomic, 256 = the tile end stores the span digests only
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128 };
+       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128, ABL_TE_DIGEST_ONLY = 256 };
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
   uint32_t* e;      // {(rel of the piece >> 4) << 8 | the lane's previous entry, gear before the piece}
@@ -533,91 +534,69 @@ __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, 
 // End of a tile: the lane's span digests; the wave's anchors, from its LDS
 // piece list, to the wave-tile's pool share in position order; the directory
 // entry and the anchor count.  Every lane walks only its own entries (a chain
-// through the list, newest first, `last` = its newest): once to count, once
-// to store, so the list costs O(entries per lane), not O(entries).  Returns a
-// lower bound of the global stores it leaves in flight, so the next round's
-// wait can leave them be.  The anchors go through `stage` (the wave's ring
-// slot of the round just read, free until the next DMA is issued): each lane
-// writes its own there, then the wave stores them with ceil(tot / 64)
-// coalesced store pairs -- a count the wave knows, so the bound is exact and
-// the next round's wait does not drain the prefetch.  (More anchors than the
-// slot holds are stored straight from the lanes and the bound is only a
-// lower one.)  A wave-tile whose list or pool share overflowed is marked for
-// the exact rescan (zc_anchor_rescan) and stores no anchors.
-constexpr uint32_t kStageAnchors = 64 * ZC_ROUND / 8;  // {rel, gear} per anchor
-__device__ __forceinline__ void lds_write32(uint8_t* p, uint32_t v) {
-  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)p;
-  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ uint32_t lds_read32(const uint8_t* p) {
-  uint32_t v;
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
-  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a) : "memory");
-  return v;
-}
+// through the list, newest first, `last` = its newest): once to count --
+// re-deriving each piece's anchor mask, kept in the entry's high half -- and
+// once to store, visiting only the set bits (each anchor's gear from the gear
+// before its dword and one v_dot4), so the list costs O(entries + anchors per
+// lane).  Returns a lower bound of the global stores it leaves in flight, so
+// the next round's wait can leave them be.  A wave-tile whose list or pool
+// share overflowed is marked for the exact rescan (zc_anchor_rescan) and
+// stores no anchors.
 template <int ABL>
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
                                                   const uint64_t (&bk)[kDigests], const WaveList& wl,
-                                                  uint32_t last, uint8_t* stage, uint64_t* __restrict__ blk,
-                                                  PoolOut po, unsigned long long* __restrict__ counters) {
+                                                  uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
+                                                  unsigned long long* __restrict__ counters) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
 #pragma unroll
   for (int t = 0; t < kDigests / 2; ++t)
     bo[t] = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
                        (uint32_t)(bk[2 * t + 1] >> 32));
+  if (ABL & ABL_TE_DIGEST_ONLY) return kDigests / 2;
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)wt * po.wcap;
-  uint32_t tot = 0, excl = 0, nst = kDigests / 2 + 2 + ((ABL & ABL_NO_ATOMIC) ? 0 : 1);
+  uint32_t tot = 0, excl = 0;
   bool over = wl.n > ZC_WLIST;
   if (!over) {
     uint32_t cnt = 0, cnt_lo = 0;  // cnt_lo: anchors in the span's first half
     for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
       const PieceHits h = piece_hits(wl, i, span0, lo_thr);
+      wl.e[2 * i] = (wl.e[2 * i] & 0xFFFFu) | (h.mask << 16);
       cnt += __popc(h.mask);
       if (h.rel < kHalfSpan) cnt_lo += __popc(h.mask);
     }
     excl = wave_excl_scan(cnt, lane, &tot);
-    tot = __builtin_amdgcn_readfirstlane(tot);
     over = tot > po.wcap;
     if (!over) {
-      const bool staged = tot <= kStageAnchors;
       // newest entry first, within each half: the first half's anchors end at
       // excl + cnt_lo, the second half's at excl + cnt (either half may be the
       // one taken first)
-      const uint32_t rbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
+      const uint32_t sbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
       uint32_t k_lo = excl + cnt_lo, k_hi = excl + cnt;
-      for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
-        const PieceHits h = piece_hits(wl, i, span0, lo_thr);
-        uint32_t& k = h.rel < kHalfSpan ? k_lo : k_hi;
-        k -= __popc(h.mask);
-        uint32_t g = h.g0, w = k;
-        for (uint32_t t = 0; t < 16; ++t) {
-          g = (g << 1) + ((h.xs[t >> 2] >> (8 * (t & 3))) & 0xFFu);
-          if ((h.mask >> t) & 1) {
-            if (staged) {
-              lds_write32(stage + 4 * w, rbase + h.rel + t);
-              lds_write32(stage + 4 * (kStageAnchors + w), g);
-            } else {
-              po.rel[base + w] = rbase + h.rel + t;
-              po.g[base + w] = g;
-            }
-            ++w;
-          }
+      for (uint32_t i = last; i != kNoEntry;) {
+        const uint32_t e0 = wl.e[2 * i];
+        const uint32_t rel = ((e0 >> 8) & 0xFFu) << 4;
+        uint32_t mask = e0 >> 16;
+        const uint4 v = wl.x[i];
+        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+        // the gear before each dword of the piece
+        uint32_t gd[4];
+        gd[0] = wl.e[2 * i + 1];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) gd[d + 1] = (gd[d] << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
+        uint32_t& k = rel < kHalfSpan ? k_lo : k_hi;
+        k -= __popc(mask);
+        for (uint32_t w = k; mask; mask &= mask - 1, ++w) {
+          const uint32_t t = __builtin_ctz(mask), d = t >> 2, q = t & 3u;
+          const uint32_t gdd = d == 0 ? gd[0] : d == 1 ? gd[1] : d == 2 ? gd[2] : gd[3];
+          const uint32_t xd = d == 0 ? xs[0] : d == 1 ? xs[1] : d == 2 ? xs[2] : xs[3];
+          // g at position t: the dword's gear shifted q + 1, plus its first q + 1
+          // bytes weighted 2^(q - j)
+          const uint32_t g = (gdd << (q + 1)) + __builtin_amdgcn_udot4(xd, 0x01020408u >> (8 * (3 - q)), 0u, false);
+          po.rel[base + w] = sbase + rel + t;
+          po.g[base + w] = g;
         }
-      }
-      if (staged) {
-        wait_lgkmcnt<0>();  // the wave's writes landed (LDS ops of a wave complete in order)
-        const uint32_t nit = (tot + 63) / 64;  // wave-uniform: one store pair each
-        for (uint32_t it = 0; it < nit; ++it) {
-          const uint32_t i = it * 64 + lane;
-          if (i < tot) {
-            const uint32_t a = lds_read32(stage + 4 * i), b = lds_read32(stage + 4 * (kStageAnchors + i));
-            wait_lgkmcnt<0>();
-            po.rel[base + i] = a;
-            po.g[base + i] = b;
-          }
-        }
-        nst += 2 * nit;
+        i = e0 & 0xFFu;
       }
     }
   }
@@ -626,7 +605,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
     po.cnt[wt] = over ? ZC_WT_OVERFLOW : tot;
     if (!(ABL & ABL_NO_ATOMIC)) atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
   }
-  return nst;
+  return kDigests / 2 + 2 + ((ABL & ABL_NO_ATOMIC) ? 0 : 1);
 }
 
 // The workgroup's rounds form one flat sequence over its tiles (32 per
@@ -732,9 +711,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     for (int p = 0; p < 4; ++p) scan_piece<ABL>(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
     wait_lgkmcnt<0>();  // the slot is free
     ties(vb);
-    // a tile's last round issues the DMA two ahead only after the tile end,
-    // which uses the slot just read to stage the anchors
-    if (R + 2 < nR && !tile_end) issue(R + 2);
+    if (R + 2 < nR) issue(R + 2);
 #pragma unroll
     for (int p = 0; p < 4; ++p)
       scan_piece<ABL>(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
@@ -745,11 +722,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (tile_end) {
-      tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, (uint8_t*)row, blk, po, counters);
-      wait_lgkmcnt<0>();  // the staging reads are done before the DMA refills the slot
-      if (R + 2 < nR) issue(R + 2);
-    }
+    if (tile_end) tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, counters);
   }
 }
 
