@@ -118,6 +118,17 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
+# chunk sizes above the 256 KiB wave-tile (a chunk's first anchor may lie in a
+# later wave-tile; horizons of 64 W), including one that is not a multiple of
+# the 1 KiB span
+@pytest.mark.parametrize("W", [262144, 300007, 1 << 20])
+def test_large_chunk_sizes_vs_oracle(torch_cuda, W):
+    spec = f"R11:{6 * W + 12345},C{3 * W + 17}:{2 * W + 999},Z:{W + 5},R12:{2 * W},C{W // 2}:{3 * W}"
+    data = oracle.gen(spec)
+    want = oracle.chunk(data, W)
+    assert _run_device(torch_cuda, data, W) == want
+
+
 # long runs of grid chunks (>= 32,768 records at once) are written by the host
 # thread pool; the runs here are cut by a same-grid match (dead refs: the
 # serial path) and by a grid-shifting one (a new epoch's run)
