@@ -118,6 +118,16 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
+# tiny chunk sizes: below the anchor offset (every ref anchorless: the exact
+# screen alone) and below the staged screen's 32-byte minimum
+@pytest.mark.parametrize("W", [1, 2, 7, 16, 31, 32, 33, 63, 64, 65])
+def test_tiny_chunk_sizes_vs_oracle(torch_cuda, W):
+    spec = "R21:20000,C333:4000,Z:700,B9:300,R22:9000,C5000:6000,R23:77"
+    data = oracle.gen(spec)
+    want = oracle.chunk(data, W)
+    assert _run_device(torch_cuda, data, W) == want
+
+
 # chunk sizes above the 256 KiB wave-tile (a chunk's first anchor may lie in a
 # later wave-tile; horizons of 64 W), including one that is not a multiple of
 # the 1 KiB span
