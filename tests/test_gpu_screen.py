@@ -82,16 +82,20 @@ def test_many_runs_per_span_overflow(torch_cuda):
     _check(torch_cuda, data, W)
 
 
-@pytest.mark.parametrize("nseeds", [1, 3, 40])
-def test_static_index_vs_oracle(torch_cuda, nseeds):
+@pytest.mark.parametrize("nseeds,nfake", [(1, 0), (3, 0), (9, 0), (40, 0), (40, 300), (40, 1900), (40, 2100)])
+def test_static_index_vs_oracle(torch_cuda, nseeds, nfake):
     # the static index (ChunkIndex::loadIndex of earlier backups) has no
     # anchors on our side: its keys go through the screen -- compared
-    # directly (1..4 keys) or through the 2^17-bit key map (more) -- and hits
-    # are confirmed by SHA-1 (chunk_index.cc:130-139)
+    # directly (1..4 keys), or the 2^17-bit key map confirmed by 16 compares
+    # (5..16) or a binary search in LDS (17..2048), or the map alone (more) --
+    # and hits are confirmed by SHA-1 (chunk_index.cc:130-139); `nfake` keys
+    # of chunks that do not occur widen the index
     W = 65536
     old = oracle.gen("R901:3000000")
     old_recs = oracle.chunk(old, W)
     seeds = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in old_recs if k == "N" and s == W][:nseeds]
+    rng = np.random.default_rng(nfake)
+    seeds += [(rng.bytes(16), int(x), W) for x in rng.integers(1, 2**63, nfake, dtype=np.int64)]
     # the new backup holds the old content at a shifted offset, plus fresh bytes
     data = np.concatenate([oracle.gen("R902:1234567"), old[: 40 * W], oracle.gen("R903:2100003"),
                            old[5 * W: 9 * W], oracle.gen("Z:700000")])

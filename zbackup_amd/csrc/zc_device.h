@@ -204,14 +204,17 @@ hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, ui
 
 // exact screen, staged: screen wave-tiles [wt0, wt0 + nwt) of ZC_FWT bytes,
 // each starting before p_end <= n (W >= 32, n >= 64), positions p in
-// [p_start, p_end); keys32 (host memory): nf <= 4 compared directly, else the
-// 2^17-bit map fbits17 (device, bit (h >> 15)); wt_cnt[wt] =
-// ZC_FWT_OVERFLOW marks a wave-tile whose runs did not fit (to be redone by
+// [p_start, p_end); the nf keys, sorted and distinct, in keys32 (host memory)
+// and d_keys32 (device): nf <= 4 compared directly; else the 2^17-bit map
+// fbits17 (device, bit (h >> 15)), whose hits are confirmed exactly for
+// nf <= 2048 (16 compares, or a binary search of the keys in LDS); wt_cnt[wt]
+// = ZC_FWT_OVERFLOW marks a wave-tile whose runs did not fit (to be redone by
 // launch_fscan)
 hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                                uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
-                               uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
-                               uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s);
+                               const uint32_t* d_keys32, uint32_t nf, const uint32_t* fbits17, Run* runs,
+                               uint64_t runs_cap, uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters,
+                               hipStream_t s);
 
 hipError_t launch_sha1(const uint8_t* data, const uint64_t* a, const uint32_t* len, uint32_t nr,
                        uint8_t* out20, hipStream_t s);

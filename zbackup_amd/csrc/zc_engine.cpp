@@ -897,14 +897,32 @@ class Resolver {
       c_.runs.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
       if (staged) {
-        HCK(launch_fscan_staged(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(), nf,
+        HCK(launch_fscan_staged(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(), c_.f32.p, nf,
                                 c_.fbits17.p, c_.runs.p, c_.runs.cap, c_.fwt_off.p, c_.fwt_cnt.p, c_.counters.p,
                                 c_.stream));
         d2h(c_, wcnt.data(), c_.fwt_cnt.p + wt_lo, wcnt.size());
         sync(c_);
-        // wave-tiles whose runs overflowed the lane slots: redo with zc_fscan
-        for (uint64_t i = 0; i < wcnt.size(); ++i)
-          if (wcnt[i] == ZC_FWT_OVERFLOW) old_screen((wt_lo + i) * kTpw, (wt_lo + i + 1) * kTpw);
+        // wave-tiles whose runs overflowed the lane slots: redo with zc_fscan,
+        // one launch per stretch of consecutive ones; a launch costs about the
+        // same for any number of tiles (a lane walks 1 KiB), so past a few
+        // stretches everything from the first to the last overflowed
+        // wave-tile is redone in one launch
+        std::vector<std::pair<uint64_t, uint64_t>> st;
+        for (uint64_t i = 0; i < wcnt.size();) {
+          if (wcnt[i] != ZC_FWT_OVERFLOW) {
+            ++i;
+            continue;
+          }
+          uint64_t j = i + 1;
+          while (j < wcnt.size() && wcnt[j] == ZC_FWT_OVERFLOW) ++j;
+          st.push_back({i, j});
+          i = j;
+        }
+        if (st.size() > 4) {
+          for (uint64_t i = st.front().first; i < st.back().second; ++i) wcnt[i] = ZC_FWT_OVERFLOW;
+          st = {{st.front().first, st.back().second}};
+        }
+        for (const auto& r : st) old_screen((wt_lo + r.first) * kTpw, (wt_lo + r.second) * kTpw);
       } else {
         old_screen(t_first, ntiles);
       }
@@ -990,18 +1008,21 @@ class Resolver {
   void build_fbatch(uint64_t p0) {
     const auto t0 = Clock::now();
     FBatch b;
-    // predicted positions: p0, p0+1..p0+7 (in case p0 fails), then the
-    // success chain p0+W, p0+2W, ... all restricted to screen runs
+    // predicted positions: the first 8 positions of every screen run from p0
+    // on (p0, p0+1.. in case p0 fails; and every later run when the runs are
+    // many short false hits of a large static index: one batch for all of
+    // them), then the success chain p0+W, p0+2W, ... restricted to the runs
     size_t save = irun_;
     std::vector<uint64_t> pos;
     uint64_t q = p0;
-    for (int k = 0; k < 8 && q != kInf; ++k) {
-      q = next_run_pos(q);
-      if (q == kInf) break;
-      pos.push_back(q);
-      ++q;
+    {
+      size_t ir = irun_;
+      while (ir < runs_.size() && runs_[ir].end <= p0) ++ir;
+      for (; ir < runs_.size() && pos.size() < kFBatchMax / 2; ++ir) {
+        const uint64_t a = std::max(p0, runs_[ir].start), b = std::min(runs_[ir].end, a + 8);
+        for (uint64_t x = a; x < b; ++x) pos.push_back(x);
+      }
     }
-    irun_ = save;
     q = p0 + W_;
     while (pos.size() < kFBatchMax) {
       q = next_run_pos(q);

@@ -1387,8 +1387,11 @@ constexpr uint32_t kFMapWords = 1u << 12;                // 2^17-bit key map, bi
 __host__ __device__ constexpr uint32_t frow_swizzle(uint32_t row) { return (row / (256 / ZC_FROUND)) % kFPieces; }
 
 struct FKeys {
-  uint32_t k[4];  // keys - 257^W (compared with V); unused slots repeat k[0]
+  uint32_t k[16];         // keys - 257^W (compared with V); unused slots repeat k[0]
+  const uint32_t* dkeys;  // NF = 32: the nk keys, sorted (copied to LDS)
+  uint32_t nk;
 };
+constexpr uint32_t kFLdsKeys = 2048;  // NF = 32: keys searched in LDS (the rest of the 160 KiB)
 
 // Rabin-Karp accumulator mod 2^32 of [a, a + W) for a, W multiples of ZC_SPAN:
 // a fold of span digests, loads batched eight at a time
@@ -1408,12 +1411,37 @@ __device__ __forceinline__ uint32_t fold_spans32(const uint64_t* __restrict__ bl
   return acc;
 }
 
+// NF = 1, 4: compares; 0: a bit of the 2^17-bit key map (false hits at
+// K / 2^17 per position); 16, 32: the map, then -- only where some lane of
+// the wave hit it -- the exact key test (false hits at K / 2^32): 16
+// compares, or a binary search of the sorted keys in LDS (K <= kFLdsKeys)
 template <int NF>
-__device__ __forceinline__ bool f_hit(uint32_t V, const FKeys& K, const uint32_t* s_map, uint32_t pw32) {
+__device__ __forceinline__ bool f_hit(uint32_t V, const FKeys& K, const uint32_t* s_map, const uint32_t* s_keys,
+                                      uint32_t pw32) {
   if (NF == 1) return V == K.k[0];
   if (NF == 4) return (V == K.k[0]) | (V == K.k[1]) | (V == K.k[2]) | (V == K.k[3]);
-  const uint32_t h = (V + pw32) >> 15;
-  return (s_map[h >> 5] >> (h & 31)) & 1u;
+  const uint32_t key = V + pw32, h = key >> 15;
+  bool hit = (s_map[h >> 5] >> (h & 31)) & 1u;
+  if (NF == 16 && __builtin_expect(__ballot(hit) != 0, 0)) {
+    bool e = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) e |= V == K.k[i];
+    hit = hit && e;
+  }
+  if (NF == 32 && __builtin_expect(__ballot(hit) != 0, 0)) {
+    uint32_t lo = 0, len = K.nk;  // lower bound of key in s_keys[0, nk)
+    while (len > 0) {
+      const uint32_t half = len >> 1;
+      if (s_keys[lo + half] < key) {
+        lo += half + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    hit = hit && lo < K.nk && s_keys[lo] == key;
+  }
+  return hit;
 }
 
 // 16-byte window at byte offset 4Q + s of the 32 bytes lo||hi
@@ -1435,11 +1463,14 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
   constexpr int kWaves = ZC_FTPB / 64;
   constexpr uint32_t kSlot = 64 * ZC_FROUND;  // bytes of one stream's round
   __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves][2][2 * kSlot];  // [slot][in | out]
-  __shared__ uint32_t s_map[NF == 0 ? kFMapWords : 1];
+  __shared__ uint32_t s_map[NF == 0 || NF == 16 || NF == 32 ? kFMapWords : 1];
+  __shared__ uint32_t s_keys[NF == 32 ? kFLdsKeys : 1];
   __shared__ uint32_t s_rs[kWaves][64 * kFRunSlots], s_re[kWaves][64 * kFRunSlots];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (NF == 0) {
+  if (NF == 0 || NF == 16 || NF == 32) {
     for (uint32_t i = tid; i < kFMapWords; i += ZC_FTPB) s_map[i] = fmap[i];
+    if (NF == 32)
+      for (uint32_t i = tid; i < K.nk; i += ZC_FTPB) s_keys[i] = K.dkeys[i];
     __syncthreads();
   }
   const uint32_t m = (uint32_t)(4 * Q) + sbyte;  // = -W mod 16
@@ -1571,7 +1602,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           V = V * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - ((xout[d] >> (8 * q)) & 0xFFu) * pw32;
-          const uint64_t b = __ballot(f_hit<NF>(V, K, s_map, pw32));
+          const uint64_t b = __ballot(f_hit<NF>(V, K, s_map, s_keys, pw32));
           any |= b;
           all &= b;
         }
@@ -1591,7 +1622,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
             for (int q = 0; q < 4; ++q) {
               Vx = Vx * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - ((xout[d] >> (8 * q)) & 0xFFu) * pw32;
               const uint64_t pos = pp + 4 * d + q;
-              const bool h = f_hit<NF>(Vx, K, s_map, pw32) && pos >= p_start && pos < p_end;
+              const bool h = f_hit<NF>(Vx, K, s_map, s_keys, pw32) && pos >= p_start && pos < p_end;
               const uint32_t rel = (uint32_t)(pos - wtbase);
               if (h && !open) {
                 open = true;
@@ -1951,6 +1982,8 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
                      sbyte, p_start, p_end, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
   if (nfk == 1) ZC_FS(1);
   else if (nfk == 4) ZC_FS(4);
+  else if (nfk == 16) ZC_FS(16);
+  else if (nfk == 32) ZC_FS(32);
   else ZC_FS(0);
 #undef ZC_FS
   return hipGetLastError();
@@ -1958,13 +1991,16 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
 
 hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                                uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, const uint32_t* keys32,
-                               uint32_t nf, const uint32_t* fbits17, Run* runs, uint64_t runs_cap,
+                               const uint32_t* d_keys32, uint32_t nf, const uint32_t* fbits17, Run* runs,
+                               uint64_t runs_cap,
                                uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
   if (W < 32 || n < 64 || p_end > n || (wt0 + nwt - 1) * ZC_FWT >= p_end || nf == 0) return hipErrorInvalidValue;
   FKeys K;
-  const int nfk = nf == 1 ? 1 : nf <= 4 ? 4 : 0;
-  for (int i = 0; i < 4; ++i) K.k[i] = (nfk != 0 ? keys32[i < (int)nf ? i : 0] : 0u) - pw32;
+  const int nfk = nf == 1 ? 1 : nf <= 4 ? 4 : nf <= 16 ? 16 : nf <= kFLdsKeys ? 32 : 0;
+  for (int i = 0; i < 16; ++i) K.k[i] = (nfk == 1 || nfk == 4 || nfk == 16 ? keys32[i < (int)nf ? i : 0] : 0u) - pw32;
+  K.dkeys = d_keys32;
+  K.nk = nfk == 32 ? nf : 0u;
   const uint32_t m = (16u - W % 16u) % 16u;
   const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * (ZC_FTPB / 64));
   const unsigned grid = (waves + ZC_FTPB / 64 - 1) / (ZC_FTPB / 64);
