@@ -244,6 +244,7 @@ struct zc_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
+  hipStream_t sha_stream = nullptr;   // SHA-1 of the grid chunks, beside the scan (ZC_FLAG_SHA1)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   std::string err;
 
@@ -266,6 +267,7 @@ struct zc_ctx {
   DevBuf<uint32_t> prel, pg, srel, sg;  // anchor pool and side pool
   DevBuf<uint32_t> otiles, obase;
   DevBuf<unsigned long long> counters;
+  DevBuf<uint8_t> gsha;  // SHA-1 of the first epoch's grid chunks (ZC_FLAG_SHA1)
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
   DevBuf<uint32_t> c_anc, c_g;
   DevBuf<uint8_t> c_dead;
@@ -349,6 +351,7 @@ class Resolver {
     if (n_ == 0) return;
     scan_upto(n_);
     HCK(launch_scan_tail(d_, n_, anchor_lo_, c_.blk.p, pool_out(), c_.counters.p, c_.stream));
+    pre_sha();
     scan_finish();
     auto t1 = std::chrono::steady_clock::now();
     // static entries keyed by rolling hash
@@ -1325,6 +1328,23 @@ class Resolver {
     nconf_ = (uint32_t)cstart_.size();
   }
 
+  // With chunk ids, the first epoch's grid chunks [k W, (k + 1) W) -- the
+  // stream's chunks unless matches move the grid -- are hashed on a side
+  // stream as soon as the bytes are in HBM (ev_in), beside the scan (the
+  // SHA-1 kernel needs no LDS, so it shares the CUs with the scan's
+  // workgroups); finalize() takes every record that is one of them from there
+  uint64_t pre_sha_n_ = 0;
+  void pre_sha() {
+    pre_sha_n_ = 0;
+    if (!(c_.flags & ZC_FLAG_SHA1) || !indexable_ || n_ < 2ull * W_) return;
+    const uint64_t k = (n_ - 2ull * W_) / W_ + 1;
+    if (k > 0xFFFFFFFFull) return;
+    c_.gsha.ensure(k * 20);
+    HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
+    HCK(launch_sha1_grid(d_, 0, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+    pre_sha_n_ = k;
+  }
+
   // ---------------------------------------------------------------- finalize
   void finalize() {
     auto t0 = Clock::now();
@@ -1350,15 +1370,26 @@ class Resolver {
     std::vector<uint64_t> h = range_digests(a, b);
     for (size_t j = 0; j < rest.size(); ++j) c_.recs[need_digest_[rest[j]].rec].rolling = h[j];
     if (c_.flags & ZC_FLAG_SHA1) {
+      std::vector<uint8_t> gsha;
+      if (pre_sha_n_) {
+        gsha.resize(pre_sha_n_ * 20);
+        HCK(hipMemcpyAsync(gsha.data(), c_.gsha.p, gsha.size(), hipMemcpyDeviceToHost, c_.sha_stream));
+        HCK(hipStreamSynchronize(c_.sha_stream));
+      }
       std::vector<uint64_t> sa;
       std::vector<uint32_t> sl;
       std::vector<size_t> idx;
-      for (size_t i = 0; i < c_.recs.size(); ++i)
-        if (c_.recs[i].kind != ZC_BYTES) {
-          sa.push_back(c_.recs[i].offset);
-          sl.push_back(c_.recs[i].size);
-          idx.push_back(i);
+      for (size_t i = 0; i < c_.recs.size(); ++i) {
+        zc_record& r = c_.recs[i];
+        if (r.kind == ZC_BYTES) continue;
+        if (r.size == W_ && r.offset % W_ == 0 && r.offset / W_ < pre_sha_n_) {
+          memcpy(r.sha1, &gsha[(r.offset / W_) * 20], 16);
+          continue;
         }
+        sa.push_back(r.offset);
+        sl.push_back(r.size);
+        idx.push_back(i);
+      }
       for (size_t off = 0; off < sa.size(); off += kFBatchMax) {
         size_t m = std::min(sa.size() - off, kFBatchMax);
         std::vector<uint64_t> pa(sa.begin() + off, sa.begin() + off + m);
@@ -1442,6 +1473,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreate(&c->ev_meta));
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
+    HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
   if (rc != ZC_OK) {
@@ -1465,6 +1497,8 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_meta) (void)hipEventDestroy(c->ev_meta);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
+    if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
+    if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -1741,13 +1741,10 @@ __device__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-__global__ void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ a,
-                               const uint32_t* __restrict__ len, uint32_t nr, uint8_t* __restrict__ out) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nr) return;
+// SHA-1 of [base, base + L) into out[20 i ..]
+__device__ void sha1_range(const uint8_t* __restrict__ data, uint64_t base, uint32_t L, uint32_t i,
+                           uint8_t* __restrict__ out) {
   uint32_t st[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
-  const uint64_t base = a[i];
-  const uint32_t L = len[i];
   uint32_t w[16];
   uint32_t full = L / 64;
   if ((base & 15) == 0) {
@@ -1814,6 +1811,19 @@ __global__ void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t*
     out[(uint64_t)i * 20 + 4 * k + 2] = v >> 8;
     out[(uint64_t)i * 20 + 4 * k + 3] = v;
   }
+}
+
+__global__ void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ a,
+                               const uint32_t* __restrict__ len, uint32_t nr, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nr) sha1_range(data, a[i], len[i], i, out);
+}
+
+// the same for the W-byte grid chunks [base0 + i W, base0 + (i + 1) W)
+__global__ void zc_sha1_grid_kernel(const uint8_t* __restrict__ data, uint64_t base0, uint32_t W, uint32_t nr,
+                                    uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nr) sha1_range(data, base0 + (uint64_t)i * W, W, i, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -2014,6 +2024,13 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
     default: return launch_fscan_staged_q<3>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                              fbits17, runs, runs_cap, wt_off, wt_cnt, counters);
   }
+}
+
+hipError_t launch_sha1_grid(const uint8_t* data, uint64_t base0, uint32_t W, uint32_t nr, uint8_t* out20,
+                            hipStream_t s) {
+  if (!nr) return hipSuccess;
+  hipLaunchKernelGGL(zc_sha1_grid_kernel, dim3(blocks_for(nr, 64)), dim3(64), 0, s, data, base0, W, nr, out20);
+  return hipGetLastError();
 }
 
 hipError_t launch_sha1(const uint8_t* data, const uint64_t* a, const uint32_t* len, uint32_t nr,
