@@ -218,8 +218,9 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
 
 hipError_t launch_sha1(const uint8_t* data, const uint64_t* a, const uint32_t* len, uint32_t nr,
                        uint8_t* out20, hipStream_t s);
-// SHA-1 of the nr W-byte chunks starting at base0, base0 + W, ... (20 bytes each)
-hipError_t launch_sha1_grid(const uint8_t* data, uint64_t base0, uint32_t W, uint32_t nr, uint8_t* out20,
+// SHA-1 (20 bytes each) of the grid chunks [i W, min((i + 1) W, n)) of an n-byte stream,
+// i < nr = ceil(n / W)
+hipError_t launch_sha1_grid(const uint8_t* data, uint64_t n, uint32_t W, uint32_t nr, uint8_t* out20,
                             hipStream_t s);
 
 hipError_t launch_fill_splitmix64(uint8_t* data, uint64_t n, uint64_t seed, hipStream_t s);

@@ -1328,7 +1328,7 @@ class Resolver {
     nconf_ = (uint32_t)cstart_.size();
   }
 
-  // With chunk ids, the first epoch's grid chunks [k W, (k + 1) W) -- the
+  // With chunk ids, the grid chunks [k W, min((k + 1) W, n)) -- the
   // stream's chunks unless matches move the grid -- are hashed on a side
   // stream as soon as the bytes are in HBM (ev_in), beside the scan (the
   // SHA-1 kernel needs no LDS, so it shares the CUs with the scan's
@@ -1336,12 +1336,12 @@ class Resolver {
   uint64_t pre_sha_n_ = 0;
   void pre_sha() {
     pre_sha_n_ = 0;
-    if (!(c_.flags & ZC_FLAG_SHA1) || !indexable_ || n_ < 2ull * W_) return;
-    const uint64_t k = (n_ - 2ull * W_) / W_ + 1;
+    if (!(c_.flags & ZC_FLAG_SHA1) || !indexable_ || n_ < W_) return;
+    const uint64_t k = (n_ + W_ - 1) / W_;
     if (k > 0xFFFFFFFFull) return;
     c_.gsha.ensure(k * 20);
     HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
-    HCK(launch_sha1_grid(d_, 0, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+    HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
     pre_sha_n_ = k;
   }
 
@@ -1382,7 +1382,7 @@ class Resolver {
       for (size_t i = 0; i < c_.recs.size(); ++i) {
         zc_record& r = c_.recs[i];
         if (r.kind == ZC_BYTES) continue;
-        if (r.size == W_ && r.offset % W_ == 0 && r.offset / W_ < pre_sha_n_) {
+        if (r.offset % W_ == 0 && r.offset / W_ < pre_sha_n_ && r.size == std::min<uint64_t>(W_, n_ - r.offset)) {
           memcpy(r.sha1, &gsha[(r.offset / W_) * 20], 16);
           continue;
         }

@@ -1714,7 +1714,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
 // zc_sha1: thread per range (FIPS 180-4)
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
 
-__device__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
+__device__ __forceinline__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = wbe[i];
@@ -1742,34 +1742,43 @@ __device__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // SHA-1 of [base, base + L) into out[20 i ..]
-__device__ void sha1_range(const uint8_t* __restrict__ data, uint64_t base, uint32_t L, uint32_t i,
+__device__ __forceinline__ void sha1_range(const uint8_t* __restrict__ data, uint64_t base, uint32_t L, uint32_t i,
                            uint8_t* __restrict__ out) {
   uint32_t st[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
   uint32_t w[16];
   uint32_t full = L / 64;
   if ((base & 15) == 0) {
-    // aligned ranges (every grid chunk): 16-byte loads, the next block's
-    // loads in flight while the current one is hashed
+    // aligned ranges (every grid chunk): 16-byte loads, kAhead blocks in
+    // flight while the current one is hashed (one block of SHA-1 is shorter
+    // than HBM's latency under load)
+    constexpr uint32_t kAhead = 4;
     const uint4* p = (const uint4*)(data + base);
-    uint4 nx[4] = {};
-    if (full) {
+    uint4 nx[kAhead][4] = {};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) nx[k] = p[k];
-    }
-    for (uint32_t blkI = 0; blkI < full; ++blkI) {
-      const uint4 cur[4] = {nx[0], nx[1], nx[2], nx[3]};
-      if (blkI + 1 < full) {
+    for (uint32_t j = 0; j < kAhead; ++j)
+      if (j < full) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) nx[k] = p[4 * (blkI + 1) + k];
+        for (int k = 0; k < 4; ++k) nx[j][k] = p[4 * j + k];
       }
+    for (uint32_t b0 = 0; b0 < full; b0 += kAhead) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        w[4 * k] = bswap32(cur[k].x);
-        w[4 * k + 1] = bswap32(cur[k].y);
-        w[4 * k + 2] = bswap32(cur[k].z);
-        w[4 * k + 3] = bswap32(cur[k].w);
+      for (uint32_t j = 0; j < kAhead; ++j) {
+        if (b0 + j < full) {
+          const uint4 cur[4] = {nx[j][0], nx[j][1], nx[j][2], nx[j][3]};
+          if (b0 + j + kAhead < full) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nx[j][k] = p[4 * (b0 + j + kAhead) + k];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            w[4 * k] = bswap32(cur[k].x);
+            w[4 * k + 1] = bswap32(cur[k].y);
+            w[4 * k + 2] = bswap32(cur[k].z);
+            w[4 * k + 3] = bswap32(cur[k].w);
+          }
+          sha1_block(st, w);
+        }
       }
-      sha1_block(st, w);
     }
   } else {
     for (uint32_t blkI = 0; blkI < full; ++blkI) {
@@ -1813,17 +1822,19 @@ __device__ void sha1_range(const uint8_t* __restrict__ data, uint64_t base, uint
   }
 }
 
-__global__ void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ a,
+__global__ __launch_bounds__(64) void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ a,
                                const uint32_t* __restrict__ len, uint32_t nr, uint8_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nr) sha1_range(data, a[i], len[i], i, out);
 }
 
-// the same for the W-byte grid chunks [base0 + i W, base0 + (i + 1) W)
-__global__ void zc_sha1_grid_kernel(const uint8_t* __restrict__ data, uint64_t base0, uint32_t W, uint32_t nr,
+// the same for the grid chunks [i W, min((i + 1) W, n)) of an n-byte stream
+__global__ __launch_bounds__(64) void zc_sha1_grid_kernel(const uint8_t* __restrict__ data, uint64_t n, uint32_t W, uint32_t nr,
                                     uint8_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nr) sha1_range(data, base0 + (uint64_t)i * W, W, i, out);
+  if (i >= nr) return;
+  const uint64_t base = (uint64_t)i * W;
+  sha1_range(data, base, (uint32_t)std::min<uint64_t>(W, n - base), i, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -2026,10 +2037,10 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
   }
 }
 
-hipError_t launch_sha1_grid(const uint8_t* data, uint64_t base0, uint32_t W, uint32_t nr, uint8_t* out20,
+hipError_t launch_sha1_grid(const uint8_t* data, uint64_t n, uint32_t W, uint32_t nr, uint8_t* out20,
                             hipStream_t s) {
-  if (!nr) return hipSuccess;
-  hipLaunchKernelGGL(zc_sha1_grid_kernel, dim3(blocks_for(nr, 64)), dim3(64), 0, s, data, base0, W, nr, out20);
+  if (!nr || !W || (uint64_t)(nr - 1) * W >= n) return nr ? hipErrorInvalidValue : hipSuccess;
+  hipLaunchKernelGGL(zc_sha1_grid_kernel, dim3(blocks_for(nr, 64)), dim3(64), 0, s, data, n, W, nr, out20);
   return hipGetLastError();
 }
 
