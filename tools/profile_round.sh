@@ -12,6 +12,7 @@ timeout -k 10 240 python3 bench.py > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
 timeout -k 10 120 python3 bench.py --config c3 --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
 timeout -k 10 120 python3 bench.py --config c5 --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
 timeout -k 10 240 python3 bench.py --e2e --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
+timeout -k 10 240 python3 bench.py --sha1 --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
 for c in c2 c3 c5; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace_$c" -o $c -- \
     python3 bench.py --config $c --steps 10 --no-cpu-baseline > "$OUT/trace_$c.log" 2>&1
