@@ -134,6 +134,17 @@ const char* zc_last_error(const zc_ctx* ctx);
  * k mod 8 of splitmix64 word k / 8, little-endian */
 int zc_fill_splitmix64(void* d_data, uint64_t n, uint64_t seed, int device);
 
+/* Whole-stream SHA-256 of the input, host side (replaces the Sha256 the feed loop
+ * keeps beside BackupCreator: sha256.hh:14-35, fed at zutils.cc:119, finished into
+ * BackupInfo.sha256 at zutils.cc:134, checked on restore at zutils.cc:225-232).
+ * One serial chain, so it runs on the host CPU (SHA extensions when present). */
+typedef struct zc_sha256 zc_sha256;
+int zc_sha256_create(zc_sha256** out);                           /* Sha256::Sha256  sha256.cc:8-11 */
+int zc_sha256_add(zc_sha256* h, const void* data, size_t n);     /* Sha256::add     sha256.cc:13-16 */
+int zc_sha256_finish(zc_sha256* h, uint8_t out[32]);             /* Sha256::finish  sha256.cc:18-21; once */
+int zc_sha256_destroy(zc_sha256* h);
+int zc_sha256_impl(const zc_sha256* h); /* 1: x86 SHA extensions, 0: scalar */
+
 int zc_abi_version(void);
 
 #ifdef __cplusplus

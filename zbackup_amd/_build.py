@@ -7,7 +7,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libzchunk.so")
-SOURCES = [os.path.join(CSRC, "zc_kernels.hip"), os.path.join(CSRC, "zc_engine.cpp")]
+SOURCES = [os.path.join(CSRC, "zc_kernels.hip"), os.path.join(CSRC, "zc_engine.cpp"),
+           os.path.join(CSRC, "zc_sha256.cpp")]
+# host-only sources (no device code; built by the host compiler with x86 intrinsics)
+HOST_ONLY = {"zc_sha256.cpp"}
 HEADERS = [os.path.join(CSRC, "zc_device.h"), os.path.join(ROOT, "include", "zchunk.h")]
 ARCH = os.environ.get("ZC_OFFLOAD_ARCH", "gfx950")
 
@@ -34,7 +37,10 @@ def build(force=False, verbose=False):
         obj = os.path.join(CSRC, os.path.basename(src) + ".o")
         cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                "-I" + os.path.join(ROOT, "include"), "-c", src, "-o", obj]
-        if src.endswith(".cpp"):
+        if os.path.basename(src) in HOST_ONLY:
+            cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I" + os.path.join(ROOT, "include"),
+                   "-c", src, "-o", obj]
+        elif src.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

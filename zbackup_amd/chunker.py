@@ -189,3 +189,44 @@ def fill_splitmix64(ptr, n, seed, device=0):
     rc = L.zc_fill_splitmix64(ctypes.c_void_p(ptr), n, seed, device)
     if rc != _lib.ZC_OK:
         raise _lib.ZcError(f"zc_fill_splitmix64 failed ({rc})")
+
+
+class Sha256:
+    """Whole-stream SHA-256 kept beside BackupCreator by the feed loop
+    (sha256.hh:14-35; fed at zutils.cc:119, finished into BackupInfo.sha256 at
+    zutils.cc:134).  Host-side, in libzchunk.so (zc_sha256_*)."""
+
+    Size = 32
+
+    def __init__(self):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        _check(self._L, None, self._L.zc_sha256_create(ctypes.byref(h)), "zc_sha256_create")
+        self._h = h
+
+    def add(self, data, size=None):
+        """Sha256::add(data, size): bytes-like data, or a host address with its size."""
+        if size is None:
+            buf = memoryview(data).cast("B")
+            arr = (ctypes.c_char * len(buf)).from_buffer_copy(buf) if buf.readonly else \
+                (ctypes.c_char * len(buf)).from_buffer(buf)
+            ptr, size = ctypes.addressof(arr), len(buf)
+        else:
+            ptr = data
+        _check(self._L, None, self._L.zc_sha256_add(self._h, ptr, size), "zc_sha256_add")
+
+    def finish(self):
+        """Sha256::finish() -> the 32-byte digest; callable once, like SHA256_Final."""
+        out = ctypes.create_string_buffer(32)
+        _check(self._L, None, self._L.zc_sha256_finish(self._h, out), "zc_sha256_finish")
+        return out.raw
+
+    @property
+    def uses_sha_extensions(self):
+        return self._L.zc_sha256_impl(self._h) == 1
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.zc_sha256_destroy(h)
+            self._h = None
