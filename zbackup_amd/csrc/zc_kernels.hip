@@ -1725,14 +1725,19 @@ __device__ __forceinline__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
     if (t < 16) {
       wt = w[t];
     } else {
-      wt = rotl32(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+      // gfx950's three-input boolean op (truth table 0x96 = x ^ y ^ z, 0xE8 =
+      // majority; both symmetric in their operands): one VALU op where the
+      // compiler emits two
+      wt = rotl32(__builtin_amdgcn_bitop3_b32(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15], 0x96) ^
+                      w[t & 15],
+                  1);
       w[t & 15] = wt;
     }
     uint32_t f, k;
     if (t < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
-    else if (t < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
-    else if (t < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8F1BBCDCu; }
-    else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+    else if (t < 40) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0x6ED9EBA1u; }
+    else if (t < 60) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8); k = 0x8F1BBCDCu; }
+    else { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0xCA62C1D6u; }
     uint32_t tmp = rotl32(a, 5) + f + e + k + wt;
     e = d; d = c; c = rotl32(b, 30); b = a; a = tmp;
   }
