@@ -1725,16 +1725,17 @@ __device__ __forceinline__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
     if (t < 16) {
       wt = w[t];
     } else {
-      // gfx950's three-input boolean op (truth table 0x96 = x ^ y ^ z, 0xE8 =
-      // majority; both symmetric in their operands): one VALU op where the
-      // compiler emits two
+      // gfx950's three-input boolean op: bit i of the table is the result for
+      // (src0, src1, src2) = bits (2, 1, 0) of i, i.e. src0/1/2 weigh 0xF0/0xCC/0xAA
+      // (0x96 = x ^ y ^ z, 0xE8 = majority, 0xCA = choose): one VALU op where the
+      // compiler emits two or three
       wt = rotl32(__builtin_amdgcn_bitop3_b32(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15], 0x96) ^
                       w[t & 15],
                   1);
       w[t & 15] = wt;
     }
     uint32_t f, k;
-    if (t < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
+    if (t < 20) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA); k = 0x5A827999u; }  // b ? c : d (src0 = 0xF0)
     else if (t < 40) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0x6ED9EBA1u; }
     else if (t < 60) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8); k = 0x8F1BBCDCu; }
     else { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0xCA62C1D6u; }
