@@ -127,11 +127,15 @@ def main():
 
     # with --sha1 a context's chunks join its index (Writer::add ->
     # ChunkIndex::addChunk), so chunking the same stream again would measure
-    # an incremental backup of identical data: every step gets a fresh
-    # context there (created before the timed region)
-    ctxs = [BackupCreator(W64, device=local, sha1=args.sha1, timing=True)
-            for _ in range(args.warmup + args.steps if args.sha1 else 1)]
-    bc = ctxs[0]
+    # an incremental backup of identical data: each step first drops them
+    # (zc_forget_stream_chunks), so every step is a first backup of the stream
+    # against the index a fresh ZBackup instance loads, on warm buffers
+    bc = BackupCreator(W64, device=local, sha1=args.sha1, timing=True)
+
+    def step():
+        if args.sha1:
+            bc.forget_stream_chunks()
+        bc.chunk_device(buf.data_ptr(), n)
 
     def barrier():
         torch.cuda.synchronize()
@@ -139,13 +143,12 @@ def main():
             dist.barrier()
 
     for k in range(args.warmup):
-        ctxs[k % len(ctxs)].chunk_device(buf.data_ptr(), n)
+        step()
     barrier()
     t0 = time.perf_counter()
     scan_ms = []
     for k in range(args.steps):
-        bc = ctxs[(args.warmup + k) % len(ctxs)]
-        bc.chunk_device(buf.data_ptr(), n)
+        step()
         scan_ms.append(bc.scan_ms())
     barrier()
     elapsed = time.perf_counter() - t0
@@ -218,8 +221,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_mib << 20, seed)
         print(json.dumps(out), flush=True)
-    for c in ctxs:
-        c.close()
+    bc.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -125,6 +125,10 @@ size_t zc_record_count(const zc_ctx* ctx);
 int zc_get_records(const zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);
 int zc_get_stats(const zc_ctx* ctx, zc_stats* out);
 int zc_reset(zc_ctx* ctx); /* begin a new stream (the seeded index is kept) */
+/* drop the index entries this context's streams added (ZC_FLAG_SHA1: Writer::add ->
+ * ChunkIndex::addChunk, chunk_storage.cc:31-46), keeping the seeded ones: the next stream
+ * sees the index a fresh ZBackup instance would load (chunk_index.cc:26-79), on warm buffers */
+int zc_forget_stream_chunks(zc_ctx* ctx);
 /* copy bytes [offset, offset+n) of the last processed stream to host memory
  * (the payload of BYTES records, for serializing bytes_to_emit) */
 int zc_read_stream(const zc_ctx* ctx, uint64_t offset, size_t n, void* host_out);

@@ -217,6 +217,31 @@ def test_index_persists_across_streams(torch_cuda):
         assert bc.record_tuples() == want_b
 
 
+def test_forget_stream_chunks_restores_the_seeded_index(torch_cuda):
+    """zc_forget_stream_chunks: after it, a stream on a reused context chunks as
+    on a fresh one with the same seeds (the stream-added entries are gone, the
+    seeded ones stay)."""
+    from zbackup_amd import BackupCreator
+    a = oracle.gen("R601:400000")
+    s = oracle.gen("R602:300000")
+    want_s = oracle.chunk(s, W64)
+    seeds = [(bytes.fromhex(sha), h, sz) for (k, o, sz, h, sha) in want_s if k == "N"]
+    b = oracle.gen("R602:300000,R601:400000,R603:5000")
+    want_b = oracle.chunk(b, W64, seeds=seeds)
+    assert any(r[0] == "D" for r in want_b)
+    with BackupCreator(W64, seeds=seeds, sha1=True) as bc:
+        for _ in range(2):
+            bc.feed(a)
+            bc.finish()
+            bc.reset()
+            bc.forget_stream_chunks()  # a's chunks leave the index again
+            bc.feed(b)
+            bc.finish()
+            assert bc.record_tuples() == want_b  # seeded matches only
+            bc.reset()
+            bc.forget_stream_chunks()
+
+
 def test_get_backup_data_matches_oracle_serialization(torch_cuda):
     from zbackup_amd import BackupCreator, chunk_id_blob, serialize_instruction
     meta, seeds, want = _case("frag50")

@@ -165,6 +165,12 @@ class BackupCreator:
         _check(self._L, self._ctx, self._L.zc_reset(self._ctx), "zc_reset")
         self._data_taken = False
 
+    def forget_stream_chunks(self):
+        """Drop the index entries this context's streams added (Writer::add ->
+        ChunkIndex::addChunk), keeping the seeded index: the next stream sees the
+        index a fresh ZBackup instance loads (chunk_index.cc:26-79)."""
+        _check(self._L, self._ctx, self._L.zc_forget_stream_chunks(self._ctx), "zc_forget_stream_chunks")
+
     def close(self):
         if self._ctx:
             self._L.zc_destroy(self._ctx)

@@ -128,6 +128,7 @@ struct HostBuf {
 struct StaticEntry {
   uint64_t key;
   uint8_t sha[16];
+  uint8_t seeded;  // 1: zc_seed_index; 0: added by one of this context's streams
 };
 
 constexpr uint64_t kInf = ~0ull;
@@ -1379,11 +1380,14 @@ class Resolver {
       std::vector<uint64_t> sa;
       std::vector<uint32_t> sl;
       std::vector<size_t> idx;
+      const bool pow2 = (W_ & (W_ - 1)) == 0;
+      const int wsh = pow2 ? __builtin_ctzll(W_) : 0;
       for (size_t i = 0; i < c_.recs.size(); ++i) {
         zc_record& r = c_.recs[i];
         if (r.kind == ZC_BYTES) continue;
-        if (r.offset % W_ == 0 && r.offset / W_ < pre_sha_n_ && r.size == std::min<uint64_t>(W_, n_ - r.offset)) {
-          memcpy(r.sha1, &gsha[(r.offset / W_) * 20], 16);
+        const uint64_t q = pow2 ? r.offset >> wsh : r.offset / W_;
+        if (q * W_ == r.offset && q < pre_sha_n_ && r.size == std::min<uint64_t>(W_, n_ - r.offset)) {
+          memcpy(r.sha1, &gsha[q * 20], 16);
           continue;
         }
         sa.push_back(r.offset);
@@ -1399,11 +1403,13 @@ class Resolver {
       }
       // Writer::add -> ChunkIndex::addChunk: later streams on this context
       // can match this stream's new chunks (only W-byte chunks can match)
+      c_.statics.reserve(c_.statics.size() + c_.recs.size());
       for (const zc_record& r : c_.recs)
         if (r.kind == ZC_CHUNK_NEW && r.size == W_) {
           StaticEntry e;
           e.key = r.rolling;
           memcpy(e.sha, r.sha1, 16);
+          e.seeded = 0;
           c_.statics.push_back(e);
         }
     }
@@ -1516,6 +1522,7 @@ int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
       StaticEntry e;
       e.key = seeds[i].rolling;
       memcpy(e.sha, seeds[i].sha1, 16);
+      e.seeded = 1;
       c->statics.push_back(e);
     }
   });
@@ -1626,6 +1633,15 @@ int zc_reset(zc_ctx* c) {
   c->recs.clear();
   c->err.clear();
   return ZC_OK;
+}
+
+int zc_forget_stream_chunks(zc_ctx* c) {
+  if (!c) return ZC_ERR_ARG;
+  return guarded(c, [&] {
+    c->statics.erase(std::remove_if(c->statics.begin(), c->statics.end(),
+                                    [](const StaticEntry& e) { return !e.seeded; }),
+                     c->statics.end());
+  });
 }
 
 int zc_read_stream(const zc_ctx* c, uint64_t offset, size_t n, void* host_out) {
