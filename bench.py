@@ -4,16 +4,30 @@
 A step = one full pass of the engine (zc_chunk_device: scan, grid keys, anchor
 probe, verification, boundary resolution, records to host) over one resident
 8 GiB synthetic stream.  Workload = BASELINE.json configs[1] (C2: 8 GiB seeded
-random bytes, W = chunk.max_size = 65536).  Multi-GPU: one process per GPU,
-each with its own independent 8 GiB stream (seed = base + rank), no
-data-path collective (configs[3]); the value is the sum of bytes over the max
-of the per-rank times.
+random bytes, W = chunk.max_size = 65536).  Multi-GPU (configs[3], C4): one
+process per GPU, each with its own independent 8 GiB stream (seed = base +
+rank), no data-path collective; the value is the sum of bytes over the max of
+the per-rank times.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5] [--e2e]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
+
+With --gpus N > 1 and no torchrun environment, this process starts N rank
+processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per child)
+before anything touches a GPU, and exits with their status; under
+`torch.distributed.run` each rank reads those variables from the environment.
+
+Besides the headline `value` (chunk ids = rolling hash, as BASELINE's metric
+names), the same line carries, driver-observed:
+  value_sha1   the same streams with complete ChunkIds (SHA-1 prefix + rolling
+               hash on every record: backup_creator.cc:130-131, chunk_id.cc:19-27)
+  end_to_end   the stream starting in pinned host memory (zc_chunk_host: H2D
+               overlapped with the scan), the zutils.cc:100-124 path
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,9 +41,10 @@ CONFIGS = {
     "c3": "C3: 8 GiB = two copies of a 4 GiB seeded random block, W=65536",
     "c5": "C5: 8 GiB all-zero stream, W=65536",
 }
+C4 = "C4: N x 8 GiB independent seeded random streams, one per GPU, W=65536"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -39,11 +54,92 @@ def parse():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-sample-mib", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--e2e", action="store_true", help="also time host(pinned)->HBM + chunking")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="headline only (skip the value_sha1 and end_to_end passes)")
+    ap.add_argument("--sha1-steps", type=int, default=5)
     ap.add_argument("--sha1", action="store_true",
-                    help="records carry SHA-1 chunk ids (ZC_FLAG_SHA1; the full chunk_to_emit content)")
-    return ap.parse_args()
+                    help="the headline itself with SHA-1 chunk ids (ZC_FLAG_SHA1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launch and rank bookkeeping: each rank chunks its "
+                         "stream with the oracle instead of the GPU (no measurement)")
+    return ap.parse_args(argv)
 
+
+# --------------------------------------------------------------------------
+# replica helpers (pure; tests/test_replicas.py runs them under gloo)
+
+def rank_seed(base, rank):
+    """Replica streams are independent: rank r chunks the stream seeded base + r
+    (BASELINE.json configs[3]: one 8 GiB buffer per GPU, seed = base + gpu)."""
+    return base + rank
+
+
+def job_max(x, world):
+    """Max of a per-rank float over the job (gloo all-reduce; identity at N=1)."""
+    if world <= 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_elapsed(elapsed, world):
+    """Whole-job time of the timed region = the max over ranks (each rank
+    brackets its own steps with a barrier and a device sync)."""
+    return job_max(elapsed, world)
+
+
+def job_gather(x, world):
+    """Per-rank values, rank order (gloo all-gather; [x] at N=1)."""
+    if world <= 1:
+        return [x]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
+def job_value(n_bytes_per_rank, world, steps, elapsed):
+    """Aggregate GiB/s: the bytes every rank chunked over the job time."""
+    return n_bytes_per_rank * world * steps / elapsed / 2**30
+
+
+def child_env(base_env, rank, world, port):
+    """Environment of rank `rank` of a self-launched N-process job."""
+    env = dict(base_env)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(argv, world, script=None, extra_env=None):
+    """Start `world` rank processes of `script` (this file) with `argv`, one per
+    GPU, and wait for all of them.  Nothing here touches a GPU: each child
+    initialises its own device.  Returns the worst exit status."""
+    script = script or os.path.abspath(__file__)
+    port = free_port()
+    base = dict(os.environ)
+    if extra_env:
+        base.update(extra_env)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=child_env(base, r, world, port))
+             for r in range(world)]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# --------------------------------------------------------------------------
 
 def cpu_baseline(sample_bytes, seed):
     """The oracle port (per-byte rotate + identity-hash hash_map probe + SHA-1
@@ -53,33 +149,7 @@ def cpu_baseline(sample_bytes, seed):
     t0 = time.perf_counter()
     recs = oracle.chunk(data, W64)
     dt = time.perf_counter() - t0
-    return {"value": round(sample_bytes / dt / 2**30, 5), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample_bytes >> 20} MiB of the C2 stream (seed {seed}), "
-                      f"{len(recs)} records in {dt:.2f} s, oracle/zc_oracle.cpp single thread",
-            "chunks_per_s": round(len(recs) / dt, 1)}
-
-
-def rank_seed(base, rank):
-    """Replica streams are independent: rank r chunks the stream seeded base + r
-    (BASELINE.json configs[3]: one 8 GiB buffer per GPU, seed = base + gpu)."""
-    return base + rank
-
-
-def job_elapsed(elapsed, world):
-    """Whole-job time of the timed region = the max over ranks (each rank
-    brackets its own steps with a barrier and a device sync)."""
-    if world <= 1:
-        return elapsed
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([elapsed], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def job_value(n_bytes_per_rank, world, steps, elapsed):
-    """Aggregate GiB/s: the bytes every rank chunked over the job time."""
-    return n_bytes_per_rank * world * steps / elapsed / 2**30
+    return {"value": sample_bytes / dt / 2**30, "seconds": dt, "records": len(recs)}
 
 
 def pmc_traffic(n_bytes):
@@ -98,94 +168,176 @@ def pmc_traffic(n_bytes):
         return None
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-
-    from zbackup_amd import BackupCreator, fill_splitmix64
-
-    n = int(args.gib * 2**30)
-    buf = torch.empty(n, dtype=torch.uint8, device=f"cuda:{local}")
-    seed = rank_seed(args.seed, rank)
-    if args.config == "c5":
+def fill_stream(torch, buf, n, config, seed, local):
+    from zbackup_amd import fill_splitmix64
+    if config == "c5":
         buf.zero_()
-    elif args.config == "c3":
+    elif config == "c3":
         fill_splitmix64(buf.data_ptr(), n // 2, seed, local)
         buf[n // 2:].copy_(buf[: n // 2])
     else:
         fill_splitmix64(buf.data_ptr(), n, seed, local)
     torch.cuda.synchronize()
 
-    # with --sha1 a context's chunks join its index (Writer::add ->
-    # ChunkIndex::addChunk), so chunking the same stream again would measure
-    # an incremental backup of identical data: each step first drops them
-    # (zc_forget_stream_chunks), so every step is a first backup of the stream
-    # against the index a fresh ZBackup instance loads, on warm buffers
-    bc = BackupCreator(W64, device=local, sha1=args.sha1, timing=True)
 
-    def step():
-        if args.sha1:
-            bc.forget_stream_chunks()
-        bc.chunk_device(buf.data_ptr(), n)
+def timed_steps(torch, world, step, warmup, steps):
+    """W untimed steps, then K timed steps between barriers + device syncs;
+    returns (job time = max over ranks, per-step scan ms of this rank)."""
+    import torch.distributed as dist
 
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    for k in range(args.warmup):
+    for _ in range(warmup):
         step()
     barrier()
     t0 = time.perf_counter()
-    scan_ms = []
-    for k in range(args.steps):
-        step()
-        scan_ms.append(bc.scan_ms())
+    scan = [step() for _ in range(steps)]
     barrier()
-    elapsed = time.perf_counter() - t0
+    return job_elapsed(time.perf_counter() - t0, world), scan
+
+
+def rank_env(args):
+    """(world, rank, local rank) from the environment; joins the gloo group
+    the replicas use for their barriers and max/gather reductions."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def dry_rank(args):
+    """--dry-run: the replica job of run_rank with the oracle (CPU) standing in
+    for the device engine, so the self-launch and the rank bookkeeping run on a
+    machine without a GPU.  Prints a line marked dry_run; not a measurement."""
+    import torch.distributed as dist
+    from oracle import oracle
+    world, rank, _ = rank_env(args)
+    n = max(int(args.gib * 2**30), 1)
+    data = oracle.splitmix64(n, rank_seed(args.seed, rank))
+    box = {}
+
+    def step():
+        box["recs"] = oracle.chunk_array(data, W64)
+        return 0.0
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = job_elapsed(time.perf_counter() - t0, world)
+    nrec = job_gather(float(len(box["recs"])), world)
+    first = job_gather(float(box["recs"]["rolling"][0]) if len(box["recs"]) else 0.0, world)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "metric": "rolling-hash chunking GiB/s (oracle rehearsal)",
+                          "value": job_value(n, world, args.steps, elapsed), "unit": "GiB/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "records_per_rank": [int(v) for v in nrec], "first_key_per_rank": first,
+                          "seeds": [rank_seed(args.seed, r) for r in range(world)]}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_rank(args):
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local = rank_env(args)
+    torch.cuda.set_device(local)
+
+    from zbackup_amd import BackupCreator
+
+    n = int(args.gib * 2**30)
+    buf = torch.empty(n, dtype=torch.uint8, device=f"cuda:{local}")
+    seed = rank_seed(args.seed, rank)
+    fill_stream(torch, buf, n, args.config, seed, local)
+
+    # with SHA-1 ids a context's chunks join its index (Writer::add ->
+    # ChunkIndex::addChunk), so chunking the same stream again would measure
+    # an incremental backup of identical data: each step first drops them
+    # (zc_forget_stream_chunks), so every step is a first backup of the stream
+    # against the index a fresh ZBackup instance loads, on warm buffers
+    def make_step(bc, sha1):
+        def step():
+            if sha1:
+                bc.forget_stream_chunks()
+            bc.chunk_device(buf.data_ptr(), n)
+            return bc.scan_ms()
+        return step
+
+    bc = BackupCreator(W64, device=local, sha1=args.sha1, timing=True)
+    elapsed, scan_ms = timed_steps(torch, world, make_step(bc, args.sha1), args.warmup, args.steps)
     st = bc.stats()
     nrec = len(bc.records())
-    elapsed = job_elapsed(elapsed, world)
+    bc.close()
     ms_step = elapsed / args.steps * 1e3
     value = job_value(n, world, args.steps, elapsed)
+    scan_avg = sum(scan_ms) / len(scan_ms)
+    fracs = [n / (s * 1e-3) / 1e9 / HBM_PEAK_GBS for s in job_gather(scan_avg, world)]
 
-    e2e = None
-    if args.e2e:
+    extras = {}
+    if not args.no_extras:
+        # complete ChunkIds on every record, same streams
+        if not args.sha1 and args.sha1_steps > 0:
+            b2 = BackupCreator(W64, device=local, sha1=True, timing=True)
+            el2, _ = timed_steps(torch, world, make_step(b2, True), 2, args.sha1_steps)
+            b2.close()
+            extras["value_sha1"] = job_value(n, world, args.sha1_steps, el2)
+            extras["sha1_ms_per_step"] = el2 / args.sha1_steps * 1e3
         # the stream starts in (pinned) host memory, as in zutils.cc:100-124
-        host = buf.cpu().pin_memory()
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        host.copy_(buf)
+        b3 = BackupCreator(W64, device=local, sha1=False, timing=True)
         reps = 3
+
+        def e2e_step():
+            b3.chunk_host(host.data_ptr(), n)
+            return 0.0
+
+        el3, _ = timed_steps(torch, world, e2e_step, 1, reps)
+        e2e = job_value(n, world, reps, el3)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(reps):
             buf.copy_(host, non_blocking=True)
         torch.cuda.synchronize()
-        h2d = n * reps / (time.perf_counter() - t1) / 2**30
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            buf.copy_(host, non_blocking=True)
-            torch.cuda.synchronize()
-            bc.chunk_device(buf.data_ptr(), n)
-        serial = n * reps / (time.perf_counter() - t1) / 2**30
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            bc.chunk_host(host.data_ptr(), n)
-        overlapped = n * reps / (time.perf_counter() - t1) / 2**30
-        e2e = {"GiB_per_s": round(overlapped, 3), "path": "pinned host buffer -> zc_chunk_host: 64 MiB H2D "
-               "segments on a side stream, each scanned as it lands, then resolve + records to host",
-               "serial_GiB_per_s": round(serial, 3), "h2d_only_GiB_per_s": round(h2d, 3)}
+        h2d = job_gather(n * reps / (time.perf_counter() - t1) / 2**30, world)
+        b3.close()
         del host
+        extras["end_to_end"] = {"value": e2e, "unit": "GiB/s", "ms_per_step": el3 / reps * 1e3,
+                                "path": "pinned host buffer -> zc_chunk_host: 64 MiB H2D segments on a side "
+                                        "stream, each scanned as it lands, then resolve + records to host",
+                                "h2d_only_GiB_per_s_per_gpu": [round(v, 2) for v in h2d]}
+
+    cpu = None
+    if not args.no_cpu_baseline and args.config == "c2":
+        # the reference path is one thread per stream (zutils.cc:100-124): N
+        # ranks run N single-thread oracle processes concurrently, one each
+        if world > 1:
+            dist.barrier()
+        c = cpu_baseline(args.cpu_sample_mib << 20, seed)
+        per = job_gather(c["value"], world)
+        cpu = {"value": round(sum(per), 5), "unit": "GiB/s", "cores": world, "kind": "port",
+               "sample": f"first {args.cpu_sample_mib} MiB of each rank's C2 stream (seed {args.seed}+rank), "
+                         f"oracle/zc_oracle.cpp single thread per rank, {world} concurrent; rank 0: "
+                         f"{c['records']} records in {c['seconds']:.2f} s",
+               "per_process": [round(v, 5) for v in per]}
 
     if rank == 0:
-        scan_avg = sum(scan_ms) / len(scan_ms)
         achieved = n / (scan_avg * 1e-3) / 1e9
         out = {
             "metric": "rolling-hash chunking GiB/s (device-resident)",
@@ -200,8 +352,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64-seeded bytes generated in HBM)",
-            "config": {"workload": CONFIGS[args.config], "stream_bytes_per_gpu": n,
-                       "chunk_max_size": W64, "parallelism": f"replicas x{world} (independent streams)",
+            "config": {"workload": C4 if world > 1 and args.config == "c2" else CONFIGS[args.config],
+                       "stream_bytes_per_gpu": n, "chunk_max_size": W64,
+                       "parallelism": f"replicas x{world} (independent streams)",
                        "chunk_ids": "SHA-1 prefix + rolling hash" if args.sha1 else "rolling hash"},
             "chunks_per_s": round(nrec * world * args.steps / elapsed, 1),
             "records_per_stream": nrec,
@@ -209,6 +362,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(n), "bytes_per_launch": n,
                          "scan_ms_avg": round(scan_avg, 4)},
+            "per_gpu_frac": [round(f, 4) for f in fracs],
             "stages": {"scan_ms": round(st["scan_ms"], 4), "resolve_ms": round(st["resolve_ms"], 4),
                        "total_ms": round(st["total_ms"], 4), "anchors": st["anchors"],
                        "candidates": st["candidates"], "epochs": st["epochs"],
@@ -216,14 +370,31 @@ def main():
                        "fscan_ms": round(st["fscan_ms"], 4), "walk_ms": round(st["walk_ms"], 4),
                        "finalize_ms": round(st["finalize_ms"], 4), "fbatch_ms": round(st["fbatch_ms"], 4)},
         }
-        if e2e:
-            out["end_to_end"] = e2e
-        if world == 1 and not args.no_cpu_baseline and args.config == "c2":
-            out["cpu_baseline"] = cpu_baseline(args.cpu_sample_mib << 20, seed)
+        if "value_sha1" in extras:
+            out["value_sha1"] = round(extras["value_sha1"], 3)
+            out["sha1_ms_per_step"] = round(extras["sha1_ms_per_step"], 3)
+        if "end_to_end" in extras:
+            e = extras["end_to_end"]
+            e["value"] = round(e["value"], 3)
+            e["ms_per_step"] = round(e["ms_per_step"], 3)
+            out["end_to_end"] = e
+        if cpu:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    bc.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # self-launched multi-GPU run: one child process per GPU
+        sys.exit(launch(sys.argv[1:], args.gpus))
+    if args.dry_run:
+        dry_rank(args)
+    else:
+        run_rank(args)
 
 
 if __name__ == "__main__":

@@ -126,8 +126,11 @@ int zc_get_records(const zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out)
 int zc_get_stats(const zc_ctx* ctx, zc_stats* out);
 int zc_reset(zc_ctx* ctx); /* begin a new stream (the seeded index is kept) */
 /* drop the index entries this context's streams added (ZC_FLAG_SHA1: Writer::add ->
- * ChunkIndex::addChunk, chunk_storage.cc:31-46), keeping the seeded ones: the next stream
- * sees the index a fresh ZBackup instance would load (chunk_index.cc:26-79), on warm buffers */
+ * ChunkIndex::addChunk, chunk_storage.cc:31-46), keeping the seeded ones.  Only for streams
+ * whose backups are DISCARDED (never committed), or for benchmarking a first backup on warm
+ * buffers: a committed backup's chunks are in its index file, which ChunkIndex::loadIndex
+ * reads on the next open (chunk_storage.cc:61-80, chunk_index.cc:26-79), so they must stay
+ * in the index (keep them, or re-seed them from the written index). */
 int zc_forget_stream_chunks(zc_ctx* ctx);
 /* copy bytes [offset, offset+n) of the last processed stream to host memory
  * (the payload of BYTES records, for serializing bytes_to_emit) */

@@ -48,6 +48,10 @@ def lib(ref=False):
     L.zco_chunk.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                             ctypes.c_size_t, ctypes.c_uint64, ctypes.POINTER(ctypes.POINTER(Record)),
                             ctypes.POINTER(ctypes.c_size_t)]
+    L.zco_chunk_ex.restype = ctypes.c_int
+    L.zco_chunk_ex.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32,
+                               ctypes.POINTER(ctypes.POINTER(Record)), ctypes.POINTER(ctypes.c_size_t)]
     L.zco_free.argtypes = [ctypes.c_void_p]
     L.zco_sha1.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     L.zco_fill_splitmix64.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
@@ -111,6 +115,36 @@ def chunk(data, W, seeds=(), feed_max=0, ref=False):
         recs.append((KIND_CHAR[r.kind], r.offset, r.size, r.rolling, bytes(r.sha1).hex()))
     L.zco_free(out)
     return recs
+
+
+RECORD_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u4"), ("kind", "<u4"),
+                         ("rolling", "<u8"), ("sha1", "u1", (16,))])
+OPT_PREFILTER = 1
+
+
+def chunk_array(data, W, seeds=(), prefilter=True):
+    """The same run as chunk(), returned as a numpy structured array laid out
+    like zc_record (for full-size comparisons).  prefilter=True puts an exact
+    key bitmap in front of the hash_map: identical records, faster misses."""
+    L = lib()
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    seed_arr = (Seed * max(len(seeds), 1))()
+    for i, (sha16, rolling, size) in enumerate(seeds):
+        seed_arr[i].sha1[:] = list(sha16)
+        seed_arr[i].rolling = rolling
+        seed_arr[i].size = size
+    out = ctypes.POINTER(Record)()
+    nout = ctypes.c_size_t()
+    rc = L.zco_chunk_ex(data.ctypes.data, data.size, W, seed_arr, len(seeds), 0,
+                        OPT_PREFILTER if prefilter else 0, ctypes.byref(out), ctypes.byref(nout))
+    if rc:
+        raise RuntimeError(f"zco_chunk_ex failed: {rc}")
+    n = nout.value
+    res = np.empty(n, dtype=RECORD_DTYPE)
+    if n:
+        ctypes.memmove(res.ctypes.data, out, n * RECORD_DTYPE.itemsize)
+    L.zco_free(out)
+    return res
 
 
 def format_records(recs):

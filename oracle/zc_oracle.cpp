@@ -99,12 +99,31 @@ class ProbeSet {
   typedef __gnu_cxx::hash_map<uint64_t, ChainLink*, IdentityHash> Map;
   Map map_;
   std::vector<ChainLink*> owned_;
+  // Optional exact prefilter (zco_chunk_ex ZCO_OPT_PREFILTER): one bit per
+  // key's low 23 bits, set on insert.  A clear bit proves the key absent, so
+  // hasKey() returns the same answer with or without it; it only saves the
+  // hash_map walk on misses (the parity tests' full-size runs use it; the timed
+  // CPU baseline does not, to keep the reference's per-byte probe cost).
+  std::vector<uint64_t> bits_;
 
  public:
+  static const unsigned kBits = 23;
   ~ProbeSet() {
     for (size_t i = 0; i < owned_.size(); ++i) delete owned_[i];
   }
+  void enablePrefilter() {
+    bits_.assign((1u << kBits) / 64, 0);
+    for (Map::iterator it = map_.begin(); it != map_.end(); ++it) setBit(it->first);
+  }
+  void setBit(uint64_t key) {
+    const uint32_t b = (uint32_t)key & ((1u << kBits) - 1);
+    bits_[b >> 6] |= 1ull << (b & 63);
+  }
   bool hasKey(uint64_t key, Map::iterator& it) {
+    if (!bits_.empty()) {
+      const uint32_t b = (uint32_t)key & ((1u << kBits) - 1);
+      if (!((bits_[b >> 6] >> (b & 63)) & 1)) return false;
+    }
     it = map_.find(key);
     return it != map_.end();
   }
@@ -115,6 +134,7 @@ class ProbeSet {
   }
   // Returns true if inserted (the id was new).
   bool add(uint64_t key, const uint8_t* sha, uint32_t size) {
+    if (!bits_.empty()) setBit(key);
     std::pair<Map::iterator, bool> r = map_.insert(std::make_pair(key, (ChainLink*)0));
     ChainLink** slot = &r.first->second;
     for (; *slot; slot = &(*slot)->next)
@@ -301,10 +321,16 @@ uint64_t zco_digest(const uint8_t* p, uint64_t n) {
 
 int zco_chunk(const uint8_t* data, uint64_t n, uint32_t W, const zco_seed* seeds,
               size_t nseeds, uint64_t feed_max, zco_record** out, size_t* nout) {
+  return zco_chunk_ex(data, n, W, seeds, nseeds, feed_max, 0, out, nout);
+}
+
+int zco_chunk_ex(const uint8_t* data, uint64_t n, uint32_t W, const zco_seed* seeds,
+                 size_t nseeds, uint64_t feed_max, uint32_t opts, zco_record** out, size_t* nout) {
   if (!out || !nout || W == 0) return -1;
   std::vector<zco_record> recs;
   {
     ProbeSet index;
+    if (opts & ZCO_OPT_PREFILTER) index.enablePrefilter();
     for (size_t i = 0; i < nseeds; ++i) index.add(seeds[i].rolling, seeds[i].sha1, seeds[i].size);
     StreamChunker ch(W, index, recs);
     uint64_t pos = 0;

@@ -36,6 +36,11 @@ typedef struct {
 uint64_t zco_digest(const uint8_t* p, uint64_t n);
 int zco_chunk(const uint8_t* data, uint64_t n, uint32_t W, const zco_seed* seeds,
               size_t nseeds, uint64_t feed_max, zco_record** out, size_t* nout);
+/* the same with options: ZCO_OPT_PREFILTER adds an exact key prefilter in
+ * front of the hash_map (identical records, faster misses) */
+enum { ZCO_OPT_PREFILTER = 1 };
+int zco_chunk_ex(const uint8_t* data, uint64_t n, uint32_t W, const zco_seed* seeds,
+                 size_t nseeds, uint64_t feed_max, uint32_t opts, zco_record** out, size_t* nout);
 void zco_free(void* p);
 void zco_sha1(const uint8_t* p, uint64_t n, uint8_t* out20);
 void zco_fill_splitmix64(uint8_t* out, uint64_t n, uint64_t seed);

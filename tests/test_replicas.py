@@ -67,3 +67,41 @@ def test_two_rank_replicas_gloo(tmp_path):
 def test_single_rank_helpers():
     assert bench.rank_seed(7, 0) == 7 and bench.rank_seed(7, 3) == 10
     assert bench.job_elapsed(1.5, 1) == 1.5
+    assert bench.job_gather(2.5, 1) == [2.5]
+    env = bench.child_env({"PATH": "/bin"}, 3, 8, 1234)
+    assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"], env["MASTER_PORT"]) == ("3", "3", "8", "1234")
+    assert env["MASTER_ADDR"] == "127.0.0.1" and env["PATH"] == "/bin"
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launches_ranks_on_cpu():
+    """`python bench.py --gpus 2` with no torchrun environment starts two rank
+    processes itself (bench.launch); --dry-run has each rank chunk its own
+    seeded stream with the oracle, so the launch, the gloo bookkeeping (max
+    over ranks, per-rank gathers) and rank 0's one JSON line run on CPU."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    out = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"),
+                          "--gpus", "2", "--dry-run", "--gib", str(2 * W / 2**30 * 64), "--steps", "2",
+                          "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0
+    assert d["seeds"] == [2024, 2025]
+    n = int(2 * W * 64)
+    assert d["records_per_rank"] == [n // 65536 + (n % 65536 > 0)] * 2
+    # independent streams: the ranks' first chunk keys differ
+    assert d["first_key_per_rank"][0] != d["first_key_per_rank"][1]
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"),
+                          "--gpus", "2", "--dry-run"], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr

@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <exception>
 #include <condition_variable>
 #include <functional>
 #include <iterator>
@@ -321,6 +322,17 @@ class Resolver {
  public:
   Resolver(zc_ctx& c, const uint8_t* d, uint64_t n)
       : c_(c), d_(d), n_(n), W_(c.W), indexable_(c.W >= 128) {}
+  // An error thrown out of the pipeline leaves no device work behind: the
+  // side streams (SHA-1 of the grid chunks, copies, tail digests) may still be
+  // reading the caller's buffer, which the caller may free once the call
+  // has returned its error.
+  ~Resolver() {
+    if (std::uncaught_exceptions() > 0) {
+      (void)hipStreamSynchronize(c_.sha_stream);
+      (void)hipStreamSynchronize(c_.copy_stream);
+      (void)hipStreamSynchronize(c_.stream);
+    }
+  }
 
   // whole pipeline over a stream already in HBM
   void run() {
