@@ -13,6 +13,8 @@
  *                          (chunk.max_size = W: zbackup.proto:79, config.cc:266-282)
  *   zc_seed_index          ChunkIndex::loadIndex -> registerNewChunkId, the static
  *                          probe set of an existing repository   chunk_index.cc:26-79,163-182
+ *   zc_set_window          the ring of W + page bytes the creator reads through
+ *                          (backup_creator.cc:28-37): the stream's bytes held in HBM
  *   zc_get_input_buffer    BackupCreator::getInputBuffer()       backup_creator.hh:78 / .cc:40-43
  *   zc_get_input_buffer_size  BackupCreator::getInputBufferSize() backup_creator.hh:79 / .cc:45-54
  *   zc_handle_more_data    BackupCreator::handleMoreData(unsigned) backup_creator.hh:81 / .cc:56-108
@@ -20,6 +22,8 @@
  *   zc_get_records         BackupCreator::getBackupData(string &) as structured records
  *                          (one per BackupInstruction, zbackup.proto:149-159)
  *                                                                backup_creator.hh:89 / .cc:275-280
+ *   zc_take_records        the same, drained as they are cut (outputInstruction,
+ *                          backup_creator.cc:267-273, runs during handleMoreData)
  *   zc_chunk_device        the same stream already resident in HBM (feed + finish in one call)
  *   zc_chunk_host          the same stream in host memory, copy overlapped with the scan
  *                          (the read loop of zutils.cc:100-124 + finish in one call)
@@ -36,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ZCHUNK_ABI_VERSION 1
+#define ZCHUNK_ABI_VERSION 2
 
 enum zc_status {
   ZC_OK = 0,
@@ -93,6 +97,10 @@ typedef struct {
   double walk_ms;        /* boundary walk + record assembly on the host */
   double finalize_ms;    /* digests of cut pieces, SHA-1 ids */
   double fbatch_ms;      /* (part of walk_ms) batched key/byte/SHA-1 checks of screen hits */
+  uint64_t window_bytes; /* feed window (zc_set_window; 0: unbounded) */
+  uint64_t hbm_bytes;    /* device memory the context holds now */
+  uint64_t segments;     /* window segments resolved during the feed */
+  uint64_t hist_entries; /* historic index entries (chunks whose bytes have left HBM) */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;
@@ -101,8 +109,23 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
 int zc_destroy(zc_ctx* ctx);
 int zc_seed_index(zc_ctx* ctx, const zc_seed* seeds, size_t n);
 
-/* host feed (zero-copy contract of BackupCreator: fill getInputBuffer() with up
- * to getInputBufferSize() bytes, then report how many were written) */
+/* Host feed (zero-copy contract of BackupCreator: fill getInputBuffer() with up
+ * to getInputBufferSize() bytes, then report how many were written).
+ *
+ * The feed streams through a bounded window (default 1 GiB, at least
+ * 8 W + 16 MiB; zc_set_window before the stream's first byte, 0 = keep the whole
+ * stream in HBM and resolve it at zc_finish): the bytes are copied to HBM as
+ * they arrive, each half window is chunked during zc_handle_more_data, and the
+ * window then slides, so device and pinned host memory stay at the window's
+ * size for a stream of any length.  Chunks whose bytes leave the window stay
+ * in the index by {rolling key, SHA-1 prefix, first content anchor} (the
+ * historic index), as the reference's index keeps ids, not bytes.
+ * Records are complete as soon as they are cut; zc_take_records drains them.
+ * The payload bytes of records taken (NEW chunks for Writer::add, BYTES for
+ * bytes_to_emit) stay readable with zc_read_stream until the next
+ * zc_get_input_buffer / zc_get_input_buffer_size / zc_feed / zc_finish call. */
+int zc_set_window(zc_ctx* ctx, uint64_t bytes);
+uint64_t zc_get_window(const zc_ctx* ctx);
 void* zc_get_input_buffer(zc_ctx* ctx);
 size_t zc_get_input_buffer_size(zc_ctx* ctx);
 int zc_handle_more_data(zc_ctx* ctx, size_t added);
@@ -121,8 +144,10 @@ int zc_chunk_device(zc_ctx* ctx, const void* d_data, uint64_t n);
  * backup_creator.cc's loop, with the feed's copies overlapped with the work */
 int zc_chunk_host(zc_ctx* ctx, const void* host, uint64_t n);
 
-size_t zc_record_count(const zc_ctx* ctx);
+size_t zc_record_count(const zc_ctx* ctx);  /* records held (cut and not yet taken) */
 int zc_get_records(const zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);
+/* move up to cap complete records out of the context, in stream order */
+int zc_take_records(zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);
 int zc_get_stats(const zc_ctx* ctx, zc_stats* out);
 int zc_reset(zc_ctx* ctx); /* begin a new stream (the seeded index is kept) */
 /* drop the index entries this context's streams added (ZC_FLAG_SHA1: Writer::add ->
@@ -133,7 +158,8 @@ int zc_reset(zc_ctx* ctx); /* begin a new stream (the seeded index is kept) */
  * in the index (keep them, or re-seed them from the written index). */
 int zc_forget_stream_chunks(zc_ctx* ctx);
 /* copy bytes [offset, offset+n) of the last processed stream to host memory
- * (the payload of BYTES records, for serializing bytes_to_emit) */
+ * (the payload of BYTES records, for serializing bytes_to_emit, and of NEW
+ * chunks, for Writer::add); for a fed stream, the bytes still in its window */
 int zc_read_stream(const zc_ctx* ctx, uint64_t offset, size_t n, void* host_out);
 const char* zc_last_error(const zc_ctx* ctx);
 

@@ -18,7 +18,7 @@ EXPORTS = ["zc_create", "zc_destroy", "zc_seed_index", "zc_get_input_buffer",
            "zc_get_input_buffer_size", "zc_handle_more_data", "zc_feed", "zc_finish",
            "zc_chunk_device", "zc_record_count", "zc_get_records", "zc_get_stats", "zc_reset",
            "zc_last_error", "zc_fill_splitmix64", "zc_abi_version", "zc_read_stream", "zc_chunk_host",
-           "zc_forget_stream_chunks", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl"]
+           "zc_forget_stream_chunks", "zc_set_window", "zc_get_window", "zc_take_records", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl"]
 
 
 class ZcRecord(ctypes.Structure):
@@ -38,7 +38,9 @@ class ZcStats(ctypes.Structure):
                 ("epochs", ctypes.c_uint64), ("fscan_runs", ctypes.c_uint64),
                 ("meta_ms", ctypes.c_double), ("probe_ms", ctypes.c_double),
                 ("fscan_ms", ctypes.c_double), ("walk_ms", ctypes.c_double),
-                ("finalize_ms", ctypes.c_double), ("fbatch_ms", ctypes.c_double)]
+                ("finalize_ms", ctypes.c_double), ("fbatch_ms", ctypes.c_double),
+                ("window_bytes", ctypes.c_uint64), ("hbm_bytes", ctypes.c_uint64),
+                ("segments", ctypes.c_uint64), ("hist_entries", ctypes.c_uint64)]
 
 
 class ZcError(RuntimeError):
@@ -77,6 +79,9 @@ def load(path=LIB_PATH):
         "zc_read_stream": (i32, [vp, u64, sz, vp]),
         "zc_chunk_host": (i32, [vp, vp, u64]),
         "zc_forget_stream_chunks": (i32, [vp]),
+        "zc_set_window": (i32, [vp, u64]),
+        "zc_get_window": (u64, [vp]),
+        "zc_take_records": (i32, [vp, ctypes.POINTER(ZcRecord), sz, ctypes.POINTER(sz)]),
         "zc_sha256_create": (i32, [ctypes.POINTER(vp)]),
         "zc_sha256_add": (i32, [vp, vp, sz]),
         "zc_sha256_finish": (i32, [vp, ctypes.c_char_p]),

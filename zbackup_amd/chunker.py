@@ -55,9 +55,12 @@ def serialize_instruction(chunk_blob=None, raw=None):
 
 class BackupCreator:
     """One stream through the engine.  `seeds` are (sha1_16, rolling, size)
-    entries of an existing index (ChunkIndex::loadIndex)."""
+    entries of an existing index (ChunkIndex::loadIndex).  `window`: bytes of
+    the feed held in HBM (None: the library's default, 1 GiB; 0: the whole
+    stream, resolved at finish()); see zc_set_window."""
 
-    def __init__(self, chunk_max_size=65536, seeds=(), device=0, sha1=True, timing=False, staged_screen=True):
+    def __init__(self, chunk_max_size=65536, seeds=(), device=0, sha1=True, timing=False, staged_screen=True,
+                 window=None):
         self._L = _lib.load()
         self.chunk_max_size = int(chunk_max_size)
         flags = (_lib.ZC_FLAG_SHA1 if sha1 else 0) | (_lib.ZC_FLAG_TIMING if timing else 0)
@@ -69,6 +72,8 @@ class BackupCreator:
             raise _lib.ZcError(f"zc_create failed ({rc})")
         self._ctx = ctx
         self._data_taken = False
+        if window is not None:
+            _check(self._L, self._ctx, self._L.zc_set_window(self._ctx, int(window)), "zc_set_window")
         seeds = list(seeds)
         if seeds:
             arr = (_lib.ZcSeed * len(seeds))()
@@ -122,6 +127,21 @@ class BackupCreator:
                self._L.zc_get_records(self._ctx, out.ctypes.data_as(ctypes.POINTER(_lib.ZcRecord)), n,
                                       ctypes.byref(got)), "zc_get_records")
         return out[: got.value]
+
+    def take_records(self):
+        """Complete records cut so far, moved out of the context (the
+        instructions outputInstruction writes during handleMoreData)."""
+        n = self._L.zc_record_count(self._ctx)
+        out = np.zeros(n, dtype=RECORD_DTYPE)
+        got = ctypes.c_size_t()
+        _check(self._L, self._ctx,
+               self._L.zc_take_records(self._ctx, out.ctypes.data_as(ctypes.POINTER(_lib.ZcRecord)), n,
+                                       ctypes.byref(got)), "zc_take_records")
+        return out[: got.value]
+
+    @property
+    def window(self):
+        return int(self._L.zc_get_window(self._ctx))
 
     def record_tuples(self):
         """(kind_char, offset, size, rolling, sha1_hex) -- the oracle's format."""

@@ -95,13 +95,16 @@ inline uint64_t wave_tiles(uint64_t n) { return (n + ZC_STILE - 1) / ZC_STILE * 
 // pool share per wave-tile: twice the expected anchor count plus slack
 inline uint32_t wave_tile_cap(uint32_t W) { return 2u * ((1u << ZC_WT_SHIFT) / anchor_rate_inv(W)) + 64u; }
 
-// where the scan writes anchors
+// where the scan writes anchors: wave-tile wt's share of the pool starts at
+// entry (wt - wt0) * wcap (wt0 = the first wave-tile of the HBM window; the
+// directory pointers base/cnt are indexed by absolute wave-tile)
 struct PoolOut {
   uint32_t* base;
   uint32_t* cnt;
   uint32_t* rel;
   uint32_t* g;
   uint32_t wcap;
+  uint64_t wt0;
 };
 
 struct Run {  // maximal run [start, end) of screen hits of the F scan
@@ -111,7 +114,7 @@ struct Run {  // maximal run [start, end) of screen hits of the F scan
 struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
   uint64_t p;
   uint32_t ref;
-  uint32_t pad;
+  uint32_t pad;  // 0: ref of the epoch, 1: historic entry `ref`
 };
 
 // Counters word layout (uint64 each)
@@ -174,13 +177,36 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                               hipStream_t s);
 uint32_t probe_filter_words();
 
+// key and first anchor of chunks [starts[i], starts[i] + W) (resident)
+hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView av, const uint64_t* starts,
+                           uint32_t cnt, uint32_t W, uint64_t pw, uint64_t* key, uint32_t* anc_off, uint32_t* cg,
+                           uint64_t* cfp, hipStream_t s);
+
+// The historic index: entries whose bytes have left HBM, {key, SHA-1 prefix}
+// on the host, {first anchor offset, gear, fingerprint} on the device; those
+// with an anchor sit in an anchor table of the epoch table's layout
+// (2^bits 16-byte slots) with its own key filter (probe_filter_words words).
+struct HistTab {
+  const uint64_t* tab;  // null: no historic entry has an anchor
+  uint32_t bits;
+  const uint32_t* filt;
+  const uint32_t* anc;  // first anchor offset per entry
+};
+// entries [e0, e0 + cnt) of g / fp into the table and its filter
+hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, uint32_t e0, uint32_t cnt, uint64_t* tab,
+                              uint32_t bits, uint32_t* filt, hipStream_t s);
+// after the window slid by `shift` pool entries: directory entries [0, cnt)
+// that point into the main pool are moved down with it
+hipError_t launch_slide_dir(uint32_t* base, const uint32_t* cnt_arr, uint32_t cnt, uint32_t shift, hipStream_t s);
+
 // every anchor of wave-tiles [wt0, wt0 + nwt) probes the filter, then the
 // table; candidate windows start at >= r (the reset point) and end before p_end
 // (the table holds every ref with an anchor; candidates name class leaders)
+// (tab may be null: the historic table alone; ht.tab null: none)
 hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
                         uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint32_t* cls,
-                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand,
-                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W,
+                        const HistTab& ht, Cand* cand, uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,

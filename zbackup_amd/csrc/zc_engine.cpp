@@ -43,6 +43,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/zchunk.h"
@@ -94,6 +95,28 @@ struct DevBuf {
     }
     cap = want;
   }
+  // grow to at least n elements (doubling), keeping the first `keep`
+  void grow_keep(size_t n, size_t keep, hipStream_t s) {
+    if (n <= cap && p) return;
+    const size_t want = std::max<size_t>(n, cap * 2);
+    T* np = nullptr;
+    hipError_t e = hipMalloc(&np, want * sizeof(T));
+    if (e != hipSuccess)
+      throw ZcError{ZC_ERR_NOMEM, std::string("hipMalloc(") + std::to_string(want * sizeof(T)) +
+                                      "): " + hipGetErrorString(e)};
+    if (keep && p) {
+      e = hipMemcpyAsync(np, p, std::min(keep, cap) * sizeof(T), hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) {
+        (void)hipFree(np);
+        throw ZcError{ZC_ERR_HIP, std::string("grow_keep: ") + hipGetErrorString(e)};
+      }
+    }
+    release();
+    p = np;
+    cap = want;
+  }
+  size_t bytes() const { return p ? cap * sizeof(T) : 0; }
 };
 
 // pinned host memory: device->host copies land here without a bounce
@@ -238,6 +261,22 @@ class HostPool {
   bool stop_ = false;
 };
 
+// an index entry known by value: (rolling key, SHA-1 prefix)
+struct IdKey {
+  uint64_t key;
+  uint8_t sha[16];
+  bool operator==(const IdKey& o) const { return key == o.key && memcmp(sha, o.sha, 16) == 0; }
+};
+struct IdKeyHash {
+  size_t operator()(const IdKey& k) const {
+    uint64_t s;
+    memcpy(&s, k.sha, 8);
+    return (size_t)(k.key ^ (s * 0x9E3779B97F4A7C15ull));
+  }
+};
+
+class Resolver;
+
 }  // namespace
 
 struct zc_ctx {
@@ -258,11 +297,41 @@ struct zc_ctx {
   const uint8_t* d_last = nullptr;  // the stream the records describe
   uint64_t n_last = 0;
 
-  std::vector<StaticEntry> statics;  // seeded index entries of size W
+  // bounded feed window (zc_set_window; 0: the whole stream is kept in HBM):
+  // stream bytes [wbase, wend) sit at dwin[0 ..) and, mirrored, in the pinned
+  // host buffer hwin that the feed writes into (getInputBuffer)
+  uint64_t win_cap = 0;
+  DevBuf<uint8_t> dwin;
+  HostBuf<uint8_t> hwin;
+  uint64_t wbase = 0, wend = 0;
+  bool slide_pending = false;  // a segment was resolved: slide before the next input
+  bool windowed_last = false;  // the last stream came through the window
+  Resolver* res = nullptr;     // the stream being fed (bounded window)
+
+  // index entries known by value: seeded ones (zc_seed_index) and this
+  // context's chunks without an anchor; probed by the exact screen
+  std::vector<StaticEntry> statics;  // entries of size W
+  std::unordered_map<uint64_t, std::vector<uint32_t>> smap;  // key -> statics
+  // historic index: this context's W-byte chunks whose bytes are gone from HBM
+  // (earlier streams, or evicted from the window), each with its first anchor
+  std::vector<uint64_t> hkey;
+  std::vector<uint8_t> hsha;  // 16 bytes per entry
+  uint32_t nhist = 0;
+  DevBuf<uint32_t> hanc, hg;
+  DevBuf<uint64_t> hfp, htab;
+  DevBuf<uint32_t> hfilt;
+  uint32_t hbits = 0;
+  std::unordered_set<IdKey, IdKeyHash> seen;  // every (key, SHA-1) of the two sets above
+
+  // records: recs holds those not yet taken (zc_take_records); the first
+  // nrec_done of them are complete (digests and chunk ids filled in)
   std::vector<zc_record, DefaultInit<zc_record>> recs;  // resize leaves new records to be written
+  size_t nrec_done = 0;
   zc_stats stats{};
 
   // scratch
+  DevBuf<uint64_t> hm_key, hm_fp;  // metadata of chunks joining the historic index
+  DevBuf<uint32_t> hm_anc, hm_g;
   DevBuf<uint64_t> blk, ftile_off;
   DevBuf<uint32_t> ftile_cnt;
   DevBuf<uint32_t> dbase, dcnt;      // anchor directory per wave-tile
@@ -318,91 +387,341 @@ void d2h(zc_ctx& c, T* dst, const T* src, size_t n) {
 void sync(zc_ctx& c) { HCK(hipStreamSynchronize(c.stream)); }
 
 // ---------------------------------------------------------------------------
+// the context's index beyond the stream being resolved
+
+void add_static(zc_ctx& c, uint64_t key, const uint8_t* sha, uint8_t seeded) {
+  StaticEntry e;
+  e.key = key;
+  memcpy(e.sha, sha, 16);
+  e.seeded = seeded;
+  c.smap[key].push_back((uint32_t)c.statics.size());
+  c.statics.push_back(e);
+}
+
+// historic table: 2^hbits >= 2 nhist slots; grows by a rebuild, otherwise
+// entries [from, nhist) are inserted
+void hist_table(zc_ctx& c, uint32_t from) {
+  if (!c.nhist) return;
+  uint32_t bits = std::max<uint32_t>(c.hbits, 12);
+  while ((1ull << bits) < 2ull * c.nhist) ++bits;
+  c.hfilt.ensure(probe_filter_words());
+  if (bits != c.hbits || !c.htab.p) {
+    sync(c);  // a probe may still read the old table
+    c.htab.ensure(2ull << bits);
+    c.hbits = bits;
+    from = 0;
+    HCK(hipMemsetAsync(c.htab.p, 0xFF, (2ull << bits) * sizeof(uint64_t), c.stream));
+    HCK(hipMemsetAsync(c.hfilt.p, 0, probe_filter_words() * sizeof(uint32_t), c.stream));
+  }
+  HCK(launch_hist_insert(c.hg.p, c.hfp.p, from, c.nhist - from, c.htab.p, c.hbits, c.hfilt.p, c.stream));
+}
+
+// append entries (their key and SHA-1 already in hkey / hsha) to the device
+// arrays and the table
+void hist_append(zc_ctx& c, const std::vector<uint32_t>& g, const std::vector<uint32_t>& anc,
+                 const std::vector<uint64_t>& fp) {
+  const uint32_t k = (uint32_t)g.size();
+  if (!k) return;
+  c.hg.grow_keep(c.nhist + k, c.nhist, c.stream);
+  c.hanc.grow_keep(c.nhist + k, c.nhist, c.stream);
+  c.hfp.grow_keep(c.nhist + k, c.nhist, c.stream);
+  h2d(c, c.hg.p + c.nhist, g.data(), k);
+  h2d(c, c.hanc.p + c.nhist, anc.data(), k);
+  h2d(c, c.hfp.p + c.nhist, fp.data(), k);
+  const uint32_t from = c.nhist;
+  c.nhist += k;
+  hist_table(c, from);
+  sync(c);  // the host vectors may go away
+}
+
+// keep the first nh historic entries and the first ns by-value entries
+void index_truncate(zc_ctx& c, uint32_t nh, size_t ns, bool force = false) {
+  if (!force && c.nhist == nh && c.statics.size() == ns) return;
+  c.nhist = std::min(c.nhist, nh);
+  c.hkey.resize(c.nhist);
+  c.hsha.resize(16 * (size_t)c.nhist);
+  if (ns < c.statics.size()) c.statics.resize(ns);
+  c.smap.clear();
+  c.seen.clear();
+  for (uint32_t i = 0; i < c.statics.size(); ++i) {
+    c.smap[c.statics[i].key].push_back(i);
+    IdKey id;
+    id.key = c.statics[i].key;
+    memcpy(id.sha, c.statics[i].sha, 16);
+    c.seen.insert(id);
+  }
+  for (uint32_t i = 0; i < c.nhist; ++i) {
+    IdKey id;
+    id.key = c.hkey[i];
+    memcpy(id.sha, &c.hsha[16 * (size_t)i], 16);
+    c.seen.insert(id);
+  }
+  c.hbits = 0;  // rebuilt
+  hist_table(c, 0);
+}
+
+// ---------------------------------------------------------------------------
 class Resolver {
  public:
-  Resolver(zc_ctx& c, const uint8_t* d, uint64_t n)
-      : c_(c), d_(d), n_(n), W_(c.W), indexable_(c.W >= 128) {}
+  // A stream of the context.  Whole-stream mode (zc_chunk_device /
+  // zc_chunk_host / an unbounded feed): the n bytes sit at `d`, and run()
+  // does everything.  Window mode (bounded feed): the stream arrives in the
+  // context's window; each full window half is resolved by run_segment()
+  // up to its last scanned tile, the window slides (rebase), and
+  // run_final() resolves the rest at finish().  All positions are absolute
+  // stream offsets: the device arrays indexed by position (the bytes, the
+  // span digests, the anchor directory, the screen's per-tile lists) are
+  // passed as pointers biased by the window base, so the kernels never see
+  // the window.
+  Resolver(zc_ctx& c, const uint8_t* d, uint64_t n, bool windowed)
+      : c_(c), dphys_(d), n_(n), cap_(windowed ? c.win_cap + ZC_STILE : n), windowed_(windowed), W_(c.W),
+        indexable_(c.W >= 128) {
+    d_ = dphys_;
+  }
   // An error thrown out of the pipeline leaves no device work behind: the
   // side streams (SHA-1 of the grid chunks, copies, tail digests) may still be
   // reading the caller's buffer, which the caller may free once the call
   // has returned its error.
   ~Resolver() {
-    if (std::uncaught_exceptions() > 0) {
-      (void)hipStreamSynchronize(c_.sha_stream);
-      (void)hipStreamSynchronize(c_.copy_stream);
-      (void)hipStreamSynchronize(c_.stream);
-    }
+    if (std::uncaught_exceptions() > 0) drain();
+  }
+  void drain() {
+    (void)hipStreamSynchronize(c_.sha_stream);
+    (void)hipStreamSynchronize(c_.copy_stream);
+    (void)hipStreamSynchronize(c_.stream);
   }
 
   // whole pipeline over a stream already in HBM
   void run() {
     begin();
-    resolve();
+    run_final();
   }
 
-  // Pipeline over a stream arriving in HBM piece by piece: begin(), then
-  // scan_upto(m) as the first m bytes land (in order, on the context's
-  // stream), then resolve() once all n bytes are queued.
+  // Stream start: statistics, records, the resolver state and the scan's
+  // buffers (sized for the window, or for the whole stream).
   void begin() {
     t_begin_ = Clock::now();
     c_.recs.clear();
-    c_.recs.reserve(std::min<uint64_t>(n_ / W_ + 16, 1u << 24));
+    c_.nrec_done = 0;
+    if (!windowed_) c_.recs.reserve(std::min<uint64_t>(n_ / W_ + 16, 1u << 24));
     c_.stats = zc_stats{};
     c_.stats.bytes = n_;
-    if (n_ == 0) return;
+    c_.stats.window_bytes = windowed_ ? c_.win_cap : 0;
+    hist0_ = c_.nhist;
+    statics0_ = c_.statics.size();
+    r_ = s_ = x_resume_ = hspan_ = 0;
     scan_setup();
   }
+  // bytes [0, n) of the stream are (being) copied to the device, in order on
+  // the context's stream
+  void set_avail(uint64_t n) {
+    n_ = n;
+    c_.stats.bytes = n;
+  }
+  // launch the scan of the full 2 MiB tiles below m
   void scan_upto(uint64_t m) {
     const uint64_t t1 = std::min(m, n_) / ZC_STILE;
     if (t1 > tiles_done_) {
-      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, c_.blk.p, pool_out(), c_.counters.p,
+      if (!scan_open_) {
+        if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
+        scan_open_ = true;
+      }
+      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
                             c_.stream));
       tiles_done_ = t1;
     }
   }
-  void resolve() {
-    if (n_ == 0) return;
-    scan_upto(n_);
-    HCK(launch_scan_tail(d_, n_, anchor_lo_, c_.blk.p, pool_out(), c_.counters.p, c_.stream));
-    pre_sha();
+  uint64_t scanned_end() const { return tiles_done_ * ZC_STILE; }
+
+  // window mode: resolve every probe below lim (the scanned end), cut the
+  // records up to there and complete them (digests, chunk ids)
+  void run_segment(uint64_t lim) {
+    const auto t0 = Clock::now();
+    scan_upto(lim);
+    lim = std::min(lim, scanned_end());
+    if (lim <= x0()) return;
     scan_finish();
-    auto t1 = std::chrono::steady_clock::now();
-    // static entries keyed by rolling hash
-    for (size_t i = 0; i < c_.statics.size(); ++i) smap_[c_.statics[i].key].push_back((uint32_t)i);
-    r_ = 0;
-    s_ = 0;
-    x_resume_ = 0;
-    hspan_ = 0;
+    lim_ = lim;
+    final_ = false;
     while (epoch()) {
     }
-    if (!scan_checked_) {  // no epoch synchronised (no refs): for the statistics
+    if (!scan_checked_) {
       sync(c_);
       scan_check();
     }
-    finalize();
-    auto t2 = std::chrono::steady_clock::now();
-    c_.stats.total_ms = std::chrono::duration<double, std::milli>(t2 - t_begin_).count();
+    finalize_records();
+    c_.stats.segments++;
+    c_.stats.total_ms += ms_since(t0);
+  }
+
+  // the end of the stream (n_ bytes): the partial last tile, every probe,
+  // finish(), the records completed; with ZC_FLAG_SHA1 the stream's new
+  // W-byte chunks join the context's index (Writer::add ->
+  // ChunkIndex::addChunk), without it the index is left as the stream found it
+  void run_final() {
+    const auto t0 = Clock::now();
+    if (n_ > 0) {
+      scan_upto(n_);
+      if (n_ % ZC_STILE && !scan_open_) {
+        if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
+        scan_open_ = true;
+      }
+      HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.counters.p, c_.stream));
+      if (!windowed_) pre_sha();
+      scan_finish();
+      lim_ = n_;
+      final_ = true;
+      while (epoch()) {
+      }
+      if (!scan_checked_) {  // no epoch synchronised (no refs): for the statistics
+        sync(c_);
+        scan_check();
+      }
+    }
+    finalize_records();
+    stream_end_index();
+    const double ms = ms_since(t0);
+    c_.stats.total_ms += ms;
     // the resolver's work overlaps the scan's tail (nothing waits for the scan
     // alone), so the part after the scan is the whole minus the scan
     c_.stats.resolve_ms = (c_.flags & ZC_FLAG_TIMING) ? std::max(0.0, c_.stats.total_ms - c_.stats.scan_ms)
-                                                      : std::chrono::duration<double, std::milli>(t2 - t1).count();
+                                                      : c_.stats.total_ms;
+    c_.stats.hist_entries = c_.nhist;
+  }
+
+  // window mode: the first stream position the resolver will read again
+  // (the next epoch's pending bytes and grid chunks from s_, the screen's
+  // and the probe's first windows from x0 - W + 1, plus one scan tile of
+  // halo for the next tile's warm-up bytes), a multiple of the 2 MiB tile
+  uint64_t keep_from() const {
+    const uint64_t xs = x0();
+    uint64_t lo = s_;
+    const uint64_t ws = xs >= W_ ? xs - W_ + 1 : 0;
+    lo = std::min(lo, (ws >> ZC_WT_SHIFT) << ZC_WT_SHIFT);
+    const uint64_t fw = xs / ZC_FWT * ZC_FWT;
+    lo = std::min(lo, fw >= (uint64_t)W_ + 4096 ? fw - W_ - 4096 : 0);
+    uint64_t keep = lo / ZC_STILE * ZC_STILE;
+    keep = keep >= ZC_STILE ? keep - ZC_STILE : 0;
+    return std::max(keep, wbase_);
+  }
+
+  // window mode: the refs that start before `keep` lose their bytes: they
+  // join the historic index (key, SHA-1, first anchor), computed now while
+  // their bytes are still resident
+  void evict_before(uint64_t keep) {
+    size_t k = 0;
+    while (k < cstart_.size() && cstart_[k] < keep) ++k;
+    if (!k) return;
+    std::vector<uint64_t> starts(cstart_.begin(), cstart_.begin() + k);
+    hist_add(starts, nullptr);
+    cstart_.erase(cstart_.begin(), cstart_.begin() + k);
+    ckey_.erase(ckey_.begin(), ckey_.begin() + k);
+    cfp_.erase(cfp_.begin(), cfp_.begin() + k);
+    cg_.erase(cg_.begin(), cg_.begin() + k);
+    canc_.erase(canc_.begin(), canc_.begin() + k);
+    nconf_ = (uint32_t)cstart_.size();
+  }
+
+  // window mode: the window moved; stream byte wbase is at dphys[0]
+  void rebase(const uint8_t* dphys, uint64_t wbase) {
+    dphys_ = dphys;
+    wbase_ = wbase;
+    d_ = dphys_ - wbase_;
+  }
+  uint64_t wbase() const { return wbase_; }
+  uint64_t chk_wt() const { return chk_wt_; }  // wave-tiles below have been checked
+
+  // New index entries from this context's chunks [starts[i], starts[i] + W)
+  // (resident): those with an anchor join the historic table, those without
+  // the by-value set of the exact screen; (key, SHA-1) pairs already indexed
+  // are skipped, as registerNewChunkId does (chunk_index.cc:163-182).
+  // sha16: the chunks' SHA-1 prefixes when known (16 bytes each), else
+  // computed here.
+  void hist_add(const std::vector<uint64_t>& starts, const uint8_t* sha16) {
+    const uint32_t k = (uint32_t)starts.size();
+    if (!k || !indexable_) return;
+    c_.va.ensure(k);
+    c_.hm_key.ensure(k);
+    c_.hm_fp.ensure(k);
+    c_.hm_anc.ensure(k);
+    c_.hm_g.ensure(k);
+    h2d(c_, c_.va.p, starts.data(), k);
+    HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, k, W_, pow257(W_), c_.hm_key.p, c_.hm_anc.p, c_.hm_g.p,
+                        c_.hm_fp.p, c_.stream));
+    std::vector<uint8_t> sha20;
+    if (!sha16) {
+      std::vector<uint32_t> len(k, W_);
+      c_.vlen.ensure(k);
+      c_.sha_out.ensure((size_t)k * 20);
+      h2d(c_, c_.vlen.p, len.data(), k);
+      HCK(launch_sha1(d_, c_.va.p, c_.vlen.p, k, c_.sha_out.p, c_.stream));
+      sha20.resize((size_t)k * 20);
+      d2h(c_, sha20.data(), c_.sha_out.p, sha20.size());
+    }
+    std::vector<uint64_t> key(k), fp(k);
+    std::vector<uint32_t> anc(k), g(k);
+    d2h(c_, key.data(), c_.hm_key.p, k);
+    d2h(c_, fp.data(), c_.hm_fp.p, k);
+    d2h(c_, anc.data(), c_.hm_anc.p, k);
+    d2h(c_, g.data(), c_.hm_g.p, k);
+    sync(c_);
+    std::vector<uint32_t> ng, nanc;
+    std::vector<uint64_t> nfp;
+    for (uint32_t i = 0; i < k; ++i) {
+      IdKey id;
+      id.key = key[i];
+      memcpy(id.sha, sha16 ? sha16 + 16 * (size_t)i : &sha20[20 * (size_t)i], 16);
+      if (!c_.seen.insert(id).second) continue;
+      if (anc[i] == ZC_NO_ANCHOR) {
+        add_static(c_, id.key, id.sha, 0);
+        continue;
+      }
+      c_.hkey.push_back(id.key);
+      c_.hsha.insert(c_.hsha.end(), id.sha, id.sha + 16);
+      ng.push_back(g[i]);
+      nanc.push_back(anc[i]);
+      nfp.push_back(fp[i]);
+    }
+    hist_append(c_, ng, nanc, nfp);
   }
 
  private:
   zc_ctx& c_;
-  const uint8_t* d_;
-  const uint64_t n_;
+  const uint8_t* dphys_;  // stream byte wbase_ is at dphys_[0]
+  const uint8_t* d_;      // dphys_ - wbase_: indexed by absolute stream offset
+  uint64_t wbase_ = 0;
+  uint64_t n_;            // bytes of the stream on the device (so far)
+  const uint64_t cap_;    // bytes the position-indexed device arrays cover
+  const bool windowed_;
+  bool final_ = true;     // this resolution reaches the end of the stream
+  uint64_t lim_ = 0;      // probes below lim_ are resolved by this call
   const uint32_t W_;
   const bool indexable_;
   uint64_t npool_ = 0;
-  uint64_t nwt_ = 0;  // wave-tiles of the stream
   const int32_t anchor_lo_ = anchor_lo_for(W_);
   const uint32_t wcap_ = wave_tile_cap(W_);
-  AnchorView av_{};
   Clock::time_point t_begin_;
   uint64_t tiles_done_ = 0;  // full scan tiles launched
+  bool scan_open_ = false;   // scan launches queued since the last scan_finish
+  uint64_t chk_wt_ = 0;      // wave-tiles below are checked for overflow
+  uint64_t side_used_ = 0;   // entries of the side pool in use
+  uint32_t hist0_ = 0;       // historic entries when the stream began
+  size_t statics0_ = 0;
 
-  PoolOut pool_out() { return PoolOut{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, wcap_}; }
+  // position-indexed device arrays, biased by the window base
+  uint64_t* blk_v() const { return c_.blk.p - wbase_ / ZC_SPAN; }
+  uint32_t* dbase_v() const { return c_.dbase.p - (wbase_ >> ZC_WT_SHIFT); }
+  uint32_t* dcnt_v() const { return c_.dcnt.p - (wbase_ >> ZC_WT_SHIFT); }
+  PoolOut pool_out() const {
+    return PoolOut{dbase_v(), dcnt_v(), c_.prel.p, c_.pg.p, wcap_, wbase_ >> ZC_WT_SHIFT};
+  }
+  AnchorView av() const { return AnchorView{dbase_v(), dcnt_v(), c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p}; }
+  HistTab hist_tab() const {
+    return c_.nhist ? HistTab{c_.htab.p, c_.hbits, c_.hfilt.p, c_.hanc.p} : HistTab{nullptr, 0, nullptr, nullptr};
+  }
+  // wave-tiles of the stream the scan has written (a partial last tile only
+  // at the end)
+  uint64_t nwt_done() const { return final_ ? wave_tiles(n_) : tiles_done_ * (ZC_SCAN_TPB / 64); }
 
   // resolver state: reset point r_, bytes saved up to s_, grid origin r_e_ of
   // the epoch (on r_'s grid: its first chunk not yet saved), its probes
@@ -468,7 +787,6 @@ class Resolver {
   std::unordered_map<uint64_t, std::vector<uint32_t>>::iterator fmemo_it_;  // last fmap_ lookup
   uint64_t fmemo_key_ = 0;
   bool fmemo_valid_ = false;
-  std::unordered_map<uint64_t, std::vector<uint32_t>> smap_;  // key -> statics
   std::vector<Run> runs_;
   uint64_t f_min_vis_ = kInf;
   bool has_f_ = false;
@@ -478,6 +796,7 @@ class Resolver {
     uint32_t ref;
   };
   std::vector<ACand> acands_;
+  std::vector<ACand> hcands_;  // confirmed candidates of historic entries (ref = entry)
 
   // F verification batch (positions ascending)
   struct FBatch {
@@ -497,17 +816,18 @@ class Resolver {
 
   // ---------------------------------------------------------------- scan
   void scan_setup() {
-    nwt_ = wave_tiles(n_);
-    if (nwt_ * wcap_ >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "stream too large for the anchor pool"};
-    c_.blk.ensure((n_ + ZC_SPAN - 1) / ZC_SPAN);
-    c_.dbase.ensure(nwt_);
-    c_.dcnt.ensure(nwt_);
-    c_.prel.ensure(nwt_ * wcap_);
-    c_.pg.ensure(nwt_ * wcap_);
+    const uint64_t nwt = wave_tiles(cap_);
+    if (nwt * wcap_ >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "stream too large for the anchor pool"};
+    c_.blk.ensure((cap_ + ZC_SPAN - 1) / ZC_SPAN);
+    c_.dbase.ensure(nwt);
+    c_.dcnt.ensure(nwt);
+    c_.prel.ensure(nwt * wcap_);
+    c_.pg.ensure(nwt * wcap_);
+    c_.srel.ensure(1);
+    c_.sg.ensure(1);
     c_.counters.ensure(CNT_LAST);
     c_.h_cnt.ensure(CNT_LAST);
     HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
-    if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
   }
 
   // The scan's counters are read back with the first epoch's batch (no
@@ -515,12 +835,10 @@ class Resolver {
   // is queued assuming no wave-tile overflowed, and redone in the rare case
   // one did (scan_check).  Overflowed wave-tiles read as empty until then.
   void scan_finish() {
-    if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev1, c_.stream));
+    meta_from_scan_ = scan_open_;
+    if ((c_.flags & ZC_FLAG_TIMING) && scan_open_) HCK(hipEventRecord(c_.ev1, c_.stream));
     c_.h_scnt.ensure(CNT_LAST);
     d2h(c_, c_.h_scnt.p, c_.counters.p, CNT_LAST);
-    c_.srel.ensure(1);
-    c_.sg.ensure(1);
-    av_ = AnchorView{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p};
     scan_checked_ = false;
   }
 
@@ -530,48 +848,58 @@ class Resolver {
   bool scan_check() {
     if (scan_checked_) return false;
     scan_checked_ = true;
-    if (c_.flags & ZC_FLAG_TIMING) {
+    if ((c_.flags & ZC_FLAG_TIMING) && scan_open_) {
       float ms = 0;
       HCK(hipEventElapsedTime(&ms, c_.ev0, c_.ev1));
-      c_.stats.scan_ms = ms;
+      c_.stats.scan_ms += ms;
     }
-    npool_ = c_.h_scnt[CNT_POOL];
-    c_.stats.anchors = npool_;
-    if (c_.h_scnt[CNT_OVERFLOW]) {
+    scan_open_ = false;
+    const uint64_t wt_lo = chk_wt_, wt_hi = nwt_done();
+    chk_wt_ = wt_hi;
+    const uint64_t found = c_.h_scnt[CNT_POOL];
+    npool_ += found;
+    c_.stats.anchors += found;
+    // the next scan launch counts from zero
+    HCK(hipMemsetAsync(c_.counters.p, 0, 2 * sizeof(unsigned long long), c_.stream));
+    if (c_.h_scnt[CNT_OVERFLOW] && wt_hi > wt_lo) {
       // wave-tiles whose anchors overflowed the scan's LDS list or their pool
       // share (dense data): count them exactly, then rescan into a side pool
-      std::vector<uint32_t> cnt(nwt_), tiles, sbase;
-      d2h(c_, cnt.data(), c_.dcnt.p, nwt_);
+      const uint64_t nw = wt_hi - wt_lo;
+      std::vector<uint32_t> cnt(nw), tiles, sbase;
+      d2h(c_, cnt.data(), dcnt_v() + wt_lo, nw);
       sync(c_);
-      for (uint64_t t = 0; t < nwt_; ++t)
-        if (cnt[t] == 0xFFFFFFFFu) tiles.push_back((uint32_t)t);
+      for (uint64_t t = 0; t < nw; ++t)
+        if (cnt[t] == 0xFFFFFFFFu) tiles.push_back((uint32_t)(wt_lo + t));
       const uint32_t nt = (uint32_t)tiles.size();
+      if (!nt) return false;
       c_.otiles.ensure(nt);
       c_.obase.ensure(nt);
       h2d(c_, c_.otiles.p, tiles.data(), nt);
-      HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, nullptr, nt, 0, c_.dbase.p, c_.dcnt.p, nullptr,
-                               nullptr, c_.stream));
-      d2h(c_, cnt.data(), c_.dcnt.p, nwt_);
+      HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, nullptr, nt, 0, dbase_v(), dcnt_v(), nullptr, nullptr,
+                               c_.stream));
+      std::vector<uint32_t> cnt2(nw);
+      d2h(c_, cnt2.data(), dcnt_v() + wt_lo, nw);
       sync(c_);
       uint64_t total = 0;
       for (uint32_t t : tiles) {
-        sbase.push_back((uint32_t)total);
-        total += cnt[t];
+        sbase.push_back((uint32_t)(side_used_ + total));
+        total += cnt2[t - wt_lo];
       }
-      if (total >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "anchor side pool too large"};
+      if (side_used_ + total >= ZC_SIDE_POOL) throw ZcError{ZC_ERR_NOMEM, "anchor side pool too large"};
       npool_ += total;
-      c_.stats.anchors = npool_;
-      c_.srel.ensure(total);
-      c_.sg.ensure(total);
+      c_.stats.anchors += total;
+      c_.srel.grow_keep(side_used_ + total, side_used_, c_.stream);
+      c_.sg.grow_keep(side_used_ + total, side_used_, c_.stream);
       h2d(c_, c_.obase.p, sbase.data(), nt);
-      HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, c_.obase.p, nt, 1, c_.dbase.p, c_.dcnt.p,
-                               c_.srel.p, c_.sg.p, c_.stream));
-      av_ = AnchorView{c_.dbase.p, c_.dcnt.p, c_.prel.p, c_.pg.p, c_.srel.p, c_.sg.p};
+      HCK(launch_anchor_rescan(d_, n_, anchor_lo_, c_.otiles.p, c_.obase.p, nt, 1, dbase_v(), dcnt_v(), c_.srel.p,
+                               c_.sg.p, c_.stream));
+      side_used_ += total;
       return true;
     }
     return false;
   }
   bool scan_checked_ = true;
+  bool meta_from_scan_ = false;  // ev1 marks the end of scan launches queued for this batch
 
   // ---------------------------------------------------------------- epoch
   // One epoch = one grid origin r_e.  Device work is queued back to back
@@ -586,7 +914,7 @@ class Resolver {
     r_e_ = s_;
     ks_ = 0;
     const uint64_t xs = x0();
-    h_end_ = hspan_ ? std::min<uint64_t>(n_, xs + hspan_) : n_;
+    h_end_ = hspan_ ? std::min<uint64_t>(lim_, xs + hspan_) : lim_;
     // grid chunks cut in the rotate phase (the last W bytes are the ring at
     // finish), and before the horizon only those cut by a probe below it
     nspec_ = (n_ >= r_e_ + 2ull * W_) ? (uint32_t)((n_ - r_e_ - 2ull * W_) / W_ + 1) : 0;
@@ -600,6 +928,7 @@ class Resolver {
     ndead_ = 0;
     cls_.clear();
     acands_.clear();
+    hcands_.clear();
     runs_.clear();
     fmap_.clear();
     fmemo_valid_ = false;
@@ -607,56 +936,65 @@ class Resolver {
     has_f_ = false;
     f_min_vis_ = kInf;
     uint64_t ncand = 0, nancless = 0;
-    if (nref_) {
+    const HistTab ht = hist_tab();
+    if (nref_ || ht.tab) {
       auto tm = Clock::now();
-      c_.c_start.ensure(nref_);
-      c_.c_key.ensure(nref_);
-      c_.c_fp.ensure(nref_);
-      c_.c_vis.ensure(nref_);
-      c_.c_anc.ensure(nref_);
-      c_.c_g.ensure(nref_);
-      c_.c_dead.ensure(nref_);
-      c_.ancless.ensure(nref_);
-      c_.h_key.ensure(nsref);
-      c_.h_cnt.ensure(CNT_LAST);
-      if (nconf_) {
-        h2d(c_, c_.c_start.p, cstart_.data(), nconf_);
-        h2d(c_, c_.c_key.p, ckey_.data(), nconf_);
-        h2d(c_, c_.c_fp.p, cfp_.data(), nconf_);
-        h2d(c_, c_.c_anc.p, canc_.data(), nconf_);
-        h2d(c_, c_.c_g.p, cg_.data(), nconf_);
-        HCK(hipMemsetAsync(c_.c_vis.p, 0, nconf_ * sizeof(uint64_t), c_.stream));
-        HCK(hipMemsetAsync(c_.c_dead.p, 0, nconf_, c_.stream));
-      }
+      const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
       uint32_t tbits = 10;  // sized for every ref having an anchor
       while ((1u << tbits) < 2u * nref_) ++tbits;
-      // content classes: identical refs share one leader in the table
-      c_.ckeys.ensure(1u << tbits);
-      c_.c_cls.ensure(nref_);
-      const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
       if (anchors) {
-        c_.tab.ensure(2u << tbits);
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
-        c_.gfilt.ensure(probe_filter_words());
+        if (nref_) {
+          c_.tab.ensure(2u << tbits);
+          c_.gfilt.ensure(probe_filter_words());
+        }
       }
-      const EpochIndex ix{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
-                          c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
-                          c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
-                          c_.gfilt.p,   c_.ancless.p, c_.counters.p};
-      HCK(launch_epoch_index(d_, n_, c_.blk.p, av_, r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
+      c_.h_cnt.ensure(CNT_LAST);
+      if (nref_) {
+        c_.c_start.ensure(nref_);
+        c_.c_key.ensure(nref_);
+        c_.c_fp.ensure(nref_);
+        c_.c_vis.ensure(nref_);
+        c_.c_anc.ensure(nref_);
+        c_.c_g.ensure(nref_);
+        c_.c_dead.ensure(nref_);
+        c_.ancless.ensure(nref_);
+        c_.h_key.ensure(nsref);
+        if (nconf_) {
+          h2d(c_, c_.c_start.p, cstart_.data(), nconf_);
+          h2d(c_, c_.c_key.p, ckey_.data(), nconf_);
+          h2d(c_, c_.c_fp.p, cfp_.data(), nconf_);
+          h2d(c_, c_.c_anc.p, canc_.data(), nconf_);
+          h2d(c_, c_.c_g.p, cg_.data(), nconf_);
+          HCK(hipMemsetAsync(c_.c_vis.p, 0, nconf_ * sizeof(uint64_t), c_.stream));
+          HCK(hipMemsetAsync(c_.c_dead.p, 0, nconf_, c_.stream));
+        }
+        // content classes: identical refs share one leader in the table
+        c_.ckeys.ensure(1u << tbits);
+        c_.c_cls.ensure(nref_);
+        const EpochIndex ix{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
+                            c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
+                            c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
+                            c_.gfilt.p,   c_.ancless.p, c_.counters.p};
+        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
+      } else {
+        HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+      }
       // the grid chunks' keys go to the host on the side stream while the
       // probe runs (the probe is queued first: nothing waits for the host to
       // set up the side stream)
       HCK(hipEventRecord(c_.ev_idx, c_.stream));
+      const uint64_t* tab = nref_ && anchors ? c_.tab.p : nullptr;
       if (anchors)
-        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
-                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, c_.cand.p, c_.cand.cap, c_.counters.p,
+                         c_.stream));
       HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
       if (nsref)
         HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c_.copy_stream));
       predict_tail();
-      const bool first = !scan_checked_;  // this batch also waits for the scan
+      const bool first = !scan_checked_ && meta_from_scan_;  // this batch also waits for the scan
       if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
@@ -665,14 +1003,15 @@ class Resolver {
         c_.stats.epochs--;
         return true;
       }
-      ncand = c_.h_cnt[CNT_CAND];
-      nancless = c_.h_cnt[CNT_ANCLESS];
-      if (c_.h_cnt[CNT_CLASS]) load_classes();
+      ncand = anchors ? c_.h_cnt[CNT_CAND] : 0;
+      nancless = nref_ ? c_.h_cnt[CNT_ANCLESS] : 0;
+      if (nref_ && c_.h_cnt[CNT_CLASS]) load_classes();
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-        HCK(launch_probe(d_, av_, pwt0(), pwt1() - pwt0(), c_.tab.p, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
-                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, c_.cand.p, c_.cand.cap, c_.counters.p, c_.stream));
+        HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, c_.cand.p, c_.cand.cap, c_.counters.p,
+                         c_.stream));
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
         ncand = c_.h_cnt[CNT_CAND];
@@ -702,8 +1041,8 @@ class Resolver {
         f_min_vis_ = std::min(f_min_vis_, ref_vis(ref));
       }
     }
-    if (!smap_.empty()) f_min_vis_ = 0;
-    if (!fmap_.empty() || !smap_.empty()) {
+    if (!c_.smap.empty()) f_min_vis_ = 0;
+    if (!fmap_.empty() || !c_.smap.empty()) {
       auto tf = Clock::now();
       fscan();
       c_.stats.fscan_ms += ms_since(tf);
@@ -724,7 +1063,7 @@ class Resolver {
     pre_a_.clear();
     pre_b_.clear();
     pre_ready_ = false;
-    if (h_end_ < n_) return;
+    if (!final_ || h_end_ < n_) return;
     const uint64_t s = nspec_ ? r_e_ + (uint64_t)nspec_ * W_ : r_e_;
     if (s >= n_) return;
     const uint64_t L = n_ - s;
@@ -744,7 +1083,7 @@ class Resolver {
     const uint32_t nr = (uint32_t)pre_a_.size();
     c_.d_pre.ensure(nr);
     c_.h_pre.ensure(nr);
-    HCK(launch_range_digest_small(d_, n_, c_.blk.p, pre_a_.data(), pre_b_.data(), nr, c_.d_pre.p, c_.copy_stream));
+    HCK(launch_range_digest_small(d_, n_, blk_v(), pre_a_.data(), pre_b_.data(), nr, c_.d_pre.p, c_.copy_stream));
     HCK(hipMemcpyAsync(c_.h_pre.p, c_.d_pre.p, nr * sizeof(uint64_t), hipMemcpyDeviceToHost, c_.copy_stream));
     pre_ready_ = true;  // read after the epoch's copy-stream synchronisation
   }
@@ -752,11 +1091,13 @@ class Resolver {
   // wave-tiles holding the anchors of windows ending in [x0, h_end)
   uint64_t pwt0() const {
     const uint64_t xs = x0();
-    return std::min<uint64_t>(nwt_, (xs >= W_ ? xs - W_ + 1 : 0) >> ZC_WT_SHIFT);
+    return std::min<uint64_t>(nwt_done(), (xs >= W_ ? xs - W_ + 1 : 0) >> ZC_WT_SHIFT);
   }
-  uint64_t pwt1() const { return std::max(pwt0(), std::min<uint64_t>(nwt_, ((h_end_ - 1) >> ZC_WT_SHIFT) + 1)); }
+  uint64_t pwt1() const { return std::max(pwt0(), std::min<uint64_t>(nwt_done(), ((h_end_ - 1) >> ZC_WT_SHIFT) + 1)); }
 
-  // byte-exact verification of every probe candidate window against its chunk
+  // every probe candidate: windows of this epoch's refs byte-exact against
+  // the ref's bytes; windows of historic entries by key and SHA-1 prefix,
+  // as ChunkIndex::findChunk confirms them (chunk_index.cc:119-143)
   void verify_candidates(uint64_t nc) {
     c_.stats.candidates += nc;
     std::vector<Cand> hc(nc);
@@ -767,8 +1108,17 @@ class Resolver {
     std::vector<uint64_t> wa, ra;
     std::vector<uint64_t> idx;
     std::vector<uint8_t> ok(nc, 1);
+    std::vector<uint64_t> ha, hb;
+    std::vector<uint64_t> hidx;
     for (uint64_t i = 0; i < nc; ++i) {
       const uint64_t ws = hc[i].p - W_ + 1;
+      if (hc[i].pad) {
+        ok[i] = 0;
+        ha.push_back(ws);
+        hb.push_back(ws + W_);
+        hidx.push_back(i);
+        continue;
+      }
       if (!cls_.empty() && ws >= r_e_ && (ws - r_e_) % W_ == 0 && (ws - r_e_) / W_ < nref_ - nconf_) {
         const uint32_t r = nconf_ + (uint32_t)((ws - r_e_) / W_);
         if (cls_[r] == hc[i].ref) continue;
@@ -779,9 +1129,33 @@ class Resolver {
     }
     std::vector<uint8_t> vok = verify_pairs(wa, ra, W_);
     for (size_t j = 0; j < idx.size(); ++j) ok[idx[j]] = vok[j];
+    if (!hidx.empty()) {
+      const std::vector<uint64_t> key = range_digests(ha, hb);
+      std::vector<uint64_t> sa;
+      std::vector<uint32_t> sl;
+      std::vector<size_t> sidx;
+      for (size_t j = 0; j < hidx.size(); ++j)
+        if (key[j] == c_.hkey[hc[hidx[j]].ref]) {
+          sa.push_back(ha[j]);
+          sl.push_back(W_);
+          sidx.push_back(j);
+        }
+      for (size_t off = 0; off < sa.size(); off += kFBatchMax) {
+        const size_t m = std::min(sa.size() - off, kFBatchMax);
+        const std::vector<uint64_t> pa(sa.begin() + off, sa.begin() + off + m);
+        const std::vector<uint32_t> pl(sl.begin() + off, sl.begin() + off + m);
+        const std::vector<uint8_t> sh = sha1s(pa, pl);
+        for (size_t j = 0; j < m; ++j) {
+          const uint64_t i = hidx[sidx[off + j]];
+          if (memcmp(&sh[20 * j], &c_.hsha[16 * (size_t)hc[i].ref], 16) == 0)
+            hcands_.push_back({hc[i].p, hc[i].ref});
+        }
+      }
+      sort_by_position(hcands_);
+    }
     acands_.reserve(nc);
     for (uint64_t i = 0; i < nc; ++i)
-      if (ok[i]) acands_.push_back({hc[i].p, hc[i].ref});
+      if (ok[i] && !hc[i].pad) acands_.push_back({hc[i].p, hc[i].ref});
     sort_by_position(acands_);
   }
 
@@ -839,7 +1213,7 @@ class Resolver {
     memcpy(c_.h_rb.p, b.data(), nr * sizeof(uint64_t));
     h2d(c_, c_.va.p, c_.h_ra.p, nr);
     h2d(c_, c_.vb.p, c_.h_rb.p, nr);
-    HCK(launch_range_digest(d_, n_, c_.blk.p, c_.va.p, c_.vb.p, (uint32_t)nr, c_.dout.p, c_.stream));
+    HCK(launch_range_digest(d_, n_, blk_v(), c_.va.p, c_.vb.p, (uint32_t)nr, c_.dout.p, c_.stream));
     d2h(c_, c_.h_rout.p, c_.dout.p, nr);
     sync(c_);
     memcpy(out.data(), c_.h_rout.p, nr * sizeof(uint64_t));
@@ -865,7 +1239,7 @@ class Resolver {
   void fscan() {
     std::vector<uint32_t> keys32;
     for (auto& kv : fmap_) keys32.push_back((uint32_t)kv.first);
-    for (auto& kv : smap_) keys32.push_back((uint32_t)kv.first);
+    for (auto& kv : c_.smap) keys32.push_back((uint32_t)kv.first);
     std::sort(keys32.begin(), keys32.end());
     keys32.erase(std::unique(keys32.begin(), keys32.end()), keys32.end());
     const uint32_t nf = (uint32_t)keys32.size();
@@ -889,34 +1263,40 @@ class Resolver {
     const uint64_t wt_lo = staged ? p_start / ZC_FWT : 0;
     const uint64_t wt_hi = staged ? (p_end + ZC_FWT - 1) / ZC_FWT : 0;
     constexpr uint64_t kTpw = ZC_FWT / ZC_TILE;  // zc_fscan tiles per screen wave-tile
-    c_.ftile_off.ensure(ntiles);
-    c_.ftile_cnt.ensure(ntiles);
-    c_.fwt_off.ensure(std::max<uint64_t>(wt_hi, 1));
-    c_.fwt_cnt.ensure(std::max<uint64_t>(wt_hi, 1));
+    // the per-tile lists are indexed by absolute tile, biased by the window base
+    const uint64_t tb = wbase_ / ZC_TILE, wb = wbase_ / ZC_FWT;
+    c_.ftile_off.ensure(ntiles - tb + 1);
+    c_.ftile_cnt.ensure(ntiles - tb + 1);
+    c_.fwt_off.ensure(std::max<uint64_t>(wt_hi, wb + 1) - wb);
+    c_.fwt_cnt.ensure(std::max<uint64_t>(wt_hi, wb + 1) - wb);
+    uint64_t* const ftile_off_v = c_.ftile_off.p - tb;
+    uint32_t* const ftile_cnt_v = c_.ftile_cnt.p - tb;
+    uint64_t* const fwt_off_v = c_.fwt_off.p - wb;
+    uint32_t* const fwt_cnt_v = c_.fwt_cnt.p - wb;
     if (staged && nf > 4) {
       std::vector<uint32_t> map17(1u << 12, 0);
       for (uint32_t h : keys32) map17[(h >> 15) >> 5] |= 1u << ((h >> 15) & 31);
       c_.fbits17.ensure(map17.size());
       h2d(c_, c_.fbits17.p, map17.data(), map17.size());
     }
-    uint64_t cap = std::max<uint64_t>(ntiles * 4, 1u << 16);
+    uint64_t cap = std::max<uint64_t>((ntiles - t_first) * 4, 1u << 16);
     unsigned long long cnt[CNT_LAST];
     auto old_screen = [&](uint64_t t0, uint64_t t1) {
       t0 = std::max(t0, t_first);
       t1 = std::min(t1, ntiles);
       if (t1 > t0)
-        HCK(launch_fscan(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
-                         c_.runs.p, c_.runs.cap, c_.ftile_off.p, c_.ftile_cnt.p, c_.counters.p, c_.stream));
+        HCK(launch_fscan(d_, n_, blk_v(), W_, pw32, p_start, p_end, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
+                         c_.runs.p, c_.runs.cap, ftile_off_v, ftile_cnt_v, c_.counters.p, c_.stream));
     };
     std::vector<uint32_t> wcnt(wt_hi - wt_lo);
     for (int attempt = 0; attempt < 3; ++attempt) {
       c_.runs.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
       if (staged) {
-        HCK(launch_fscan_staged(d_, n_, c_.blk.p, W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(), c_.f32.p, nf,
-                                c_.fbits17.p, c_.runs.p, c_.runs.cap, c_.fwt_off.p, c_.fwt_cnt.p, c_.counters.p,
-                                c_.stream));
-        d2h(c_, wcnt.data(), c_.fwt_cnt.p + wt_lo, wcnt.size());
+        HCK(launch_fscan_staged(d_, n_, blk_v(), W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(),
+                                c_.f32.p, nf, c_.fbits17.p, c_.runs.p, c_.runs.cap, fwt_off_v, fwt_cnt_v,
+                                c_.counters.p, c_.stream));
+        d2h(c_, wcnt.data(), fwt_cnt_v + wt_lo, wcnt.size());
         sync(c_);
         // wave-tiles whose runs overflowed the lane slots: redo with zc_fscan,
         // one launch per stretch of consecutive ones; a launch costs about the
@@ -954,14 +1334,14 @@ class Resolver {
     bool old_ran = !staged;
     for (uint32_t c : wcnt) old_ran |= c == ZC_FWT_OVERFLOW;
     std::vector<Run> raw(nruns);
-    std::vector<uint64_t> toff(old_ran ? ntiles : 0), woff(wcnt.size());
-    std::vector<uint32_t> tcnt(old_ran ? ntiles : 0);
+    std::vector<uint64_t> toff(old_ran ? ntiles - t_first : 0), woff(wcnt.size());
+    std::vector<uint32_t> tcnt(old_ran ? ntiles - t_first : 0);
     d2h(c_, raw.data(), c_.runs.p, nruns);
     if (old_ran) {
-      d2h(c_, toff.data(), c_.ftile_off.p, ntiles);
-      d2h(c_, tcnt.data(), c_.ftile_cnt.p, ntiles);
+      d2h(c_, toff.data(), ftile_off_v + t_first, ntiles - t_first);
+      d2h(c_, tcnt.data(), ftile_cnt_v + t_first, ntiles - t_first);
     }
-    d2h(c_, woff.data(), c_.fwt_off.p + wt_lo, woff.size());
+    d2h(c_, woff.data(), fwt_off_v + wt_lo, woff.size());
     sync(c_);
     auto take = [&](const Run* q, uint64_t k) {
       for (uint64_t i = 0; i < k; ++i) {
@@ -972,7 +1352,8 @@ class Resolver {
       }
     };
     auto take_tiles = [&](uint64_t t0, uint64_t t1) {
-      for (uint64_t t = std::max(t0, t_first); t < std::min(t1, ntiles); ++t) take(&raw[toff[t]], tcnt[t]);
+      for (uint64_t t = std::max(t0, t_first); t < std::min(t1, ntiles); ++t)
+        take(&raw[toff[t - t_first]], tcnt[t - t_first]);
     };
     if (!staged) take_tiles(t_first, ntiles);
     for (uint64_t i = 0; i < wcnt.size(); ++i) {
@@ -1068,7 +1449,7 @@ class Resolver {
     b.pos = std::move(pos);
     b.vref.assign(np, -1);
     b.vok.assign(np, 0);
-    const bool statics = !smap_.empty();
+    const bool statics = !c_.smap.empty();
     b.has_sha.assign(statics ? np : 0, 0);
     b.sha.assign(statics ? np * 20 : 0, 0);
     std::vector<uint64_t> wa, ra;
@@ -1088,7 +1469,7 @@ class Resolver {
           widx.push_back(i);
         }
       }
-      if (statics && smap_.count(b.h[i])) {
+      if (statics && c_.smap.count(b.h[i])) {
         sa.push_back(a[i]);
         sl.push_back(W_);
         sidx.push_back(i);
@@ -1133,8 +1514,8 @@ class Resolver {
       }
     }
     // static index entries: SHA-1 prefix of the window (chunk_index.cc:130-139)
-    auto st = smap_.find(h);
-    if (st != smap_.end()) {
+    auto st = c_.smap.find(h);
+    if (st != c_.smap.end()) {
       if (!fb_.has_sha[i]) {
         std::vector<uint64_t> sa{p - W_ + 1};
         std::vector<uint32_t> sl{W_};
@@ -1252,16 +1633,27 @@ class Resolver {
     return true;
   }
 
+  // the probes of this epoch are done up to h_end_: go on at a horizon, stop
+  // at the end of a window segment (the state carries over to the next one),
+  // or finish the stream
+  bool stop() {
+    if (h_end_ < lim_) return horizon_stop();
+    if (!final_) {
+      save_grid_until(h_end_ - 1);
+      keep_saved(h_end_ - 1);
+      x_resume_ = h_end_;
+      return false;
+    }
+    finish();
+    return false;
+  }
+
   bool walk() {
     uint64_t x = x0();
-    size_t ia = 0;
+    size_t ia = 0, ih = 0;
     irun_ = 0;
     for (;;) {
-      if (x >= h_end_) {
-        if (h_end_ < n_) return horizon_stop();
-        finish();
-        return false;
-      }
+      if (x >= h_end_) return stop();
       uint64_t pa = kInf;
       uint32_t refa = 0;
       while (ia < acands_.size()) {
@@ -1273,20 +1665,23 @@ class Resolver {
         }
         ++ia;
       }
+      // historic entries are always in the index
+      while (ih < hcands_.size() && hcands_[ih].p < x) ++ih;
+      const uint64_t ph = ih < hcands_.size() ? hcands_[ih].p : kInf;
+      const uint64_t pe = std::min(pa, ph);
       uint64_t fkey = 0;
-      uint64_t pf = next_f(x, pa == kInf ? h_end_ : pa + 1, &fkey);
-      if (pa == kInf && pf == kInf) {
-        if (h_end_ < n_) return horizon_stop();
-        finish();
-        return false;
-      }
+      uint64_t pf = next_f(x, pe == kInf ? h_end_ : pe + 1, &fkey);
+      if (pe == kInf && pf == kInf) return stop();
       uint64_t m, key;
-      if (pf != kInf && (pa == kInf || pf < pa)) {
+      if (pf != kInf && (pe == kInf || pf < pe)) {
         m = pf;
         key = fkey;
-      } else {
+      } else if (pa <= ph) {
         m = pa;
         key = ref_key(refa);
+      } else {
+        m = ph;
+        key = c_.hkey[hcands_[ih].ref];
       }
       // the match at m
       save_grid_until(m);
@@ -1359,7 +1754,11 @@ class Resolver {
   }
 
   // ---------------------------------------------------------------- finalize
-  void finalize() {
+  // Records [nrec_done, size) are complete once their pieces have digests
+  // and (ZC_FLAG_SHA1) every chunk record its SHA-1 prefix.
+  std::vector<uint64_t> fresh_;  // NEW W-byte chunks of the stream still resident: offset,
+  std::vector<uint8_t> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
+  void finalize_records() {
     auto t0 = Clock::now();
     struct Done {
       zc_stats& st;
@@ -1382,6 +1781,8 @@ class Resolver {
     }
     std::vector<uint64_t> h = range_digests(a, b);
     for (size_t j = 0; j < rest.size(); ++j) c_.recs[need_digest_[rest[j]].rec].rolling = h[j];
+    need_digest_.clear();
+    const size_t r0 = c_.nrec_done;
     if (c_.flags & ZC_FLAG_SHA1) {
       std::vector<uint8_t> gsha;
       if (pre_sha_n_) {
@@ -1394,7 +1795,7 @@ class Resolver {
       std::vector<size_t> idx;
       const bool pow2 = (W_ & (W_ - 1)) == 0;
       const int wsh = pow2 ? __builtin_ctzll(W_) : 0;
-      for (size_t i = 0; i < c_.recs.size(); ++i) {
+      for (size_t i = r0; i < c_.recs.size(); ++i) {
         zc_record& r = c_.recs[i];
         if (r.kind == ZC_BYTES) continue;
         const uint64_t q = pow2 ? r.offset >> wsh : r.offset / W_;
@@ -1413,18 +1814,41 @@ class Resolver {
         std::vector<uint8_t> sh = sha1s(pa, pl);
         for (size_t j = 0; j < m; ++j) memcpy(c_.recs[idx[off + j]].sha1, &sh[j * 20], 16);
       }
-      // Writer::add -> ChunkIndex::addChunk: later streams on this context
-      // can match this stream's new chunks (only W-byte chunks can match)
-      c_.statics.reserve(c_.statics.size() + c_.recs.size());
-      for (const zc_record& r : c_.recs)
+      for (size_t i = r0; i < c_.recs.size(); ++i) {
+        const zc_record& r = c_.recs[i];
         if (r.kind == ZC_CHUNK_NEW && r.size == W_) {
-          StaticEntry e;
-          e.key = r.rolling;
-          memcpy(e.sha, r.sha1, 16);
-          e.seeded = 0;
-          c_.statics.push_back(e);
+          fresh_.push_back(r.offset);
+          fresh_sha_.insert(fresh_sha_.end(), r.sha1, r.sha1 + 16);
         }
+      }
     }
+    c_.nrec_done = c_.recs.size();
+  }
+
+  // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
+  // context's index (Writer::add -> ChunkIndex::addChunk, chunk_storage.cc:
+  // 31-46): a later stream on this context matches them, as a later backup
+  // matches a committed one's index (chunk_index.cc:26-79).  Without it the
+  // index is left as the stream found it (entries evicted from the window
+  // during the stream are dropped again).
+  void stream_end_index() {
+    if (c_.flags & ZC_FLAG_SHA1) {
+      hist_add(fresh_, fresh_sha_.data());
+    } else {
+      index_truncate(c_, hist0_, statics0_);
+    }
+    fresh_.clear();
+    fresh_sha_.clear();
+  }
+
+ public:
+  // window mode: NEW chunks below `keep` are no longer resident; those that
+  // are refs went to the historic index with evict_before()
+  void drop_fresh_before(uint64_t keep) {
+    size_t k = 0;
+    while (k < fresh_.size() && fresh_[k] < keep) ++k;
+    fresh_.erase(fresh_.begin(), fresh_.begin() + k);
+    fresh_sha_.erase(fresh_sha_.begin(), fresh_sha_.begin() + 16 * k);
   }
 };
 
@@ -1468,6 +1892,112 @@ void append_device(zc_ctx& c, const void* src, size_t n, hipMemcpyKind kind) {
   c.n_stream += n;
 }
 
+// ---------------------------------------------------------------------------
+// The bounded feed window (zc_set_window).  The feed writes into the pinned
+// host mirror at the window's end (getInputBuffer), each piece is copied to
+// the same place in HBM on the copy stream, and once half a window of new
+// bytes has arrived the resolver takes every probe up to the last full scan
+// tile (run_segment).  Before the next input the window slides down to what
+// the resolver will read again (Resolver::keep_from: about 2 W + 4 MiB),
+// moving the bytes, their span digests and anchors with it; chunks that
+// start below that join the historic index first.  HBM and pinned memory
+// stay at the window's size however long the stream is.
+constexpr uint64_t kDefaultWindow = 1ull << 30;
+constexpr uint64_t kFeedMax = 64ull << 20;  // most bytes one getInputBuffer offers
+
+uint64_t window_for(uint64_t want, uint32_t W) {
+  // a window half must hold new tiles beyond what the resolver keeps
+  const uint64_t m = std::max<uint64_t>(want, 8ull * W + (16ull << 20));
+  return (m + ZC_STILE - 1) / ZC_STILE * ZC_STILE;
+}
+
+void window_open(zc_ctx& c) {
+  if (c.res) return;
+  c.dwin.ensure(c.win_cap);
+  c.hwin.ensure(c.win_cap);
+  c.wbase = c.wend = 0;
+  c.windowed_last = true;
+  c.res = new Resolver(c, c.dwin.p, 0, true);
+  c.res->begin();
+}
+
+void window_close(zc_ctx& c) {
+  delete c.res;
+  c.res = nullptr;
+  c.slide_pending = false;
+}
+
+// buf[shift, shift + len) -> buf[0, len), in stream order, pieces no longer
+// than the shift so no piece overlaps its own source
+template <class T>
+void move_down(hipStream_t s, T* buf, uint64_t shift, uint64_t len) {
+  if (!shift || !len) return;
+  for (uint64_t off = 0; off < len; off += shift) {
+    const uint64_t m = std::min(shift, len - off);
+    HCK(hipMemcpyAsync(buf + off, buf + off + shift, m * sizeof(T), hipMemcpyDeviceToDevice, s));
+  }
+}
+
+void window_slide(zc_ctx& c) {
+  c.slide_pending = false;
+  Resolver& r = *c.res;
+  const uint64_t keep = r.keep_from();
+  if (keep <= c.wbase) return;
+  r.evict_before(keep);
+  r.drop_fresh_before(keep);
+  HCK(hipStreamWaitEvent(c.stream, c.ev_in, 0));  // the window's copies have landed
+  const uint64_t sh = keep - c.wbase, len = c.wend - keep;
+  move_down(c.stream, c.dwin.p, sh, len);
+  // span digests and anchors of the scanned tiles above `keep`
+  const uint64_t scanned = std::max(r.scanned_end(), keep);
+  move_down(c.stream, c.blk.p, sh / ZC_SPAN, (scanned - keep) / ZC_SPAN);
+  const uint64_t w0 = sh >> ZC_WT_SHIFT, wl = (scanned - keep) >> ZC_WT_SHIFT;
+  const uint64_t wcap = wave_tile_cap(c.W);
+  move_down(c.stream, c.dbase.p, w0, wl);
+  move_down(c.stream, c.dcnt.p, w0, wl);
+  move_down(c.stream, c.prel.p, w0 * wcap, wl * wcap);
+  move_down(c.stream, c.pg.p, w0 * wcap, wl * wcap);
+  HCK(launch_slide_dir(c.dbase.p, c.dcnt.p, (uint32_t)wl, (uint32_t)(w0 * wcap), c.stream));
+  HCK(hipStreamSynchronize(c.copy_stream));
+  memmove(c.hwin.p, c.hwin.p + sh, len);
+  c.wbase = keep;
+  r.rebase(c.dwin.p, keep);
+  sync(c);
+}
+
+size_t window_room(const zc_ctx& c) {
+  return (size_t)std::min<uint64_t>(kFeedMax, c.win_cap - (c.wend - c.wbase));
+}
+
+void window_add(zc_ctx& c, size_t added) {
+  const uint64_t off = c.wend - c.wbase;
+  if (added > c.win_cap - off) throw ZcError{ZC_ERR_ARG, "handleMoreData: more than getInputBufferSize() bytes"};
+  if (!added) return;
+  HCK(hipMemcpyAsync(c.dwin.p + off, c.hwin.p + off, added, hipMemcpyHostToDevice, c.copy_stream));
+  HCK(hipEventRecord(c.ev_in, c.copy_stream));
+  HCK(hipStreamWaitEvent(c.stream, c.ev_in, 0));
+  c.wend += added;
+  c.res->set_avail(c.wend);
+  if (c.wend - c.res->scanned_end() >= c.win_cap / 2) {
+    c.res->run_segment(c.wend / ZC_STILE * ZC_STILE);
+    c.slide_pending = true;
+  }
+}
+
+size_t ctx_hbm_bytes(const zc_ctx& c) {
+  size_t b = c.d_stream.bytes() + c.dwin.bytes() + c.hanc.bytes() + c.hg.bytes() + c.hfp.bytes() + c.htab.bytes() +
+             c.hfilt.bytes() + c.hm_key.bytes() + c.hm_fp.bytes() + c.hm_anc.bytes() + c.hm_g.bytes() +
+             c.blk.bytes() + c.ftile_off.bytes() + c.ftile_cnt.bytes() + c.dbase.bytes() + c.dcnt.bytes() +
+             c.prel.bytes() + c.pg.bytes() + c.srel.bytes() + c.sg.bytes() + c.otiles.bytes() + c.obase.bytes() +
+             c.counters.bytes() + c.gsha.bytes() + c.c_start.bytes() + c.c_key.bytes() + c.c_fp.bytes() +
+             c.c_vis.bytes() + c.c_anc.bytes() + c.c_g.bytes() + c.c_dead.bytes() + c.ckeys.bytes() +
+             c.c_cls.bytes() + c.tab.bytes() + c.gfilt.bytes() + c.cand.bytes() + c.va.bytes() + c.vb.bytes() +
+             c.dout.bytes() + c.vlen.bytes() + c.vok.bytes() + c.sha_out.bytes() + c.f32.bytes() + c.fbits.bytes() +
+             c.fbits17.bytes() + c.fwt_off.bytes() + c.fwt_cnt.bytes() + c.runs.bytes() + c.ancless.bytes() +
+             c.d_pre.bytes();
+  return b;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1482,6 +2012,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
   c->device = device;
   c->W = chunk_max_size;
   c->flags = flags;
+  c->win_cap = window_for(kDefaultWindow, chunk_max_size);
   int rc = guarded(c, [&] {
     DeviceGuard g(device);
     HCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -1509,6 +2040,7 @@ int zc_destroy(zc_ctx* c) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    window_close(*c);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1531,43 +2063,114 @@ int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
   return guarded(c, [&] {
     for (size_t i = 0; i < n; ++i) {
       if (seeds[i].size != c->W) continue;  // only W-byte entries can equal a W-byte window
-      StaticEntry e;
-      e.key = seeds[i].rolling;
-      memcpy(e.sha, seeds[i].sha1, 16);
-      e.seeded = 1;
-      c->statics.push_back(e);
+      IdKey id;
+      id.key = seeds[i].rolling;
+      memcpy(id.sha, seeds[i].sha1, 16);
+      if (!c->seen.insert(id).second) continue;  // registerNewChunkId: already indexed
+      add_static(*c, id.key, id.sha, 1);
     }
   });
 }
 
-void* zc_get_input_buffer(zc_ctx* c) { return (c && !c->finished) ? c->stage : nullptr; }
+int zc_set_window(zc_ctx* c, uint64_t bytes) {
+  if (!c) return ZC_ERR_ARG;
+  if (c->res || c->n_stream) return ZC_ERR_STATE;
+  c->win_cap = bytes ? window_for(bytes, c->W) : 0;
+  return ZC_OK;
+}
 
-size_t zc_get_input_buffer_size(zc_ctx* c) { return (c && !c->finished) ? kFeedChunk : 0; }
+uint64_t zc_get_window(const zc_ctx* c) { return c ? c->win_cap : 0; }
+
+void* zc_get_input_buffer(zc_ctx* c) {
+  if (!c || c->finished) return nullptr;
+  if (!c->win_cap) return c->stage;
+  void* p = nullptr;
+  int rc = guarded(c, [&] {
+    DeviceGuard g(c->device);
+    window_open(*c);
+    if (c->slide_pending) window_slide(*c);
+    p = c->hwin.p + (c->wend - c->wbase);
+  });
+  return rc == ZC_OK ? p : nullptr;
+}
+
+size_t zc_get_input_buffer_size(zc_ctx* c) {
+  if (!c || c->finished) return 0;
+  if (!c->win_cap) return kFeedChunk;
+  size_t n = 0;
+  int rc = guarded(c, [&] {
+    DeviceGuard g(c->device);
+    window_open(*c);
+    if (c->slide_pending) window_slide(*c);
+    n = window_room(*c);
+  });
+  return rc == ZC_OK ? n : 0;
+}
 
 int zc_handle_more_data(zc_ctx* c, size_t added) {
-  if (!c || added > kFeedChunk) return ZC_ERR_ARG;
+  if (!c) return ZC_ERR_ARG;
   if (c->finished) return ZC_ERR_STATE;
+  if (!c->win_cap) {
+    if (added > kFeedChunk) return ZC_ERR_ARG;
+    return guarded(c, [&] {
+      DeviceGuard g(c->device);
+      append_device(*c, c->stage, added, hipMemcpyHostToDevice);
+    });
+  }
+  if (!c->res) return ZC_ERR_STATE;  // no getInputBuffer() before it
   return guarded(c, [&] {
     DeviceGuard g(c->device);
-    append_device(*c, c->stage, added, hipMemcpyHostToDevice);
+    window_add(*c, added);
   });
 }
 
 int zc_feed(zc_ctx* c, const void* host, size_t n) {
   if (!c || (n && !host)) return ZC_ERR_ARG;
   if (c->finished) return ZC_ERR_STATE;
-  return guarded(c, [&] {
-    DeviceGuard g(c->device);
-    append_device(*c, host, n, hipMemcpyHostToDevice);
-  });
+  if (!c->win_cap) {
+    return guarded(c, [&] {
+      DeviceGuard g(c->device);
+      append_device(*c, host, n, hipMemcpyHostToDevice);
+    });
+  }
+  const uint8_t* h = (const uint8_t*)host;
+  while (n) {
+    uint8_t* dst = (uint8_t*)zc_get_input_buffer(c);
+    const size_t room = zc_get_input_buffer_size(c);
+    if (!dst || !room) return dst ? ZC_ERR_STATE : (c->err.empty() ? ZC_ERR_STATE : ZC_ERR_HIP);
+    const size_t m = std::min(room, n);
+    memcpy(dst, h, m);
+    const int rc = zc_handle_more_data(c, m);
+    if (rc != ZC_OK) return rc;
+    h += m;
+    n -= m;
+  }
+  return ZC_OK;
 }
 
 int zc_finish(zc_ctx* c) {
   if (!c) return ZC_ERR_ARG;
   if (c->finished) return ZC_ERR_STATE;
+  if (c->win_cap) {
+    return guarded(c, [&] {
+      DeviceGuard g(c->device);
+      window_open(*c);
+      try {
+        c->res->run_final();
+      } catch (...) {
+        window_close(*c);
+        throw;
+      }
+      window_close(*c);
+      c->d_last = c->dwin.p;
+      c->n_last = c->wend;
+      c->finished = true;
+    });
+  }
   return guarded(c, [&] {
     DeviceGuard g(c->device);
-    Resolver res(*c, c->d_stream.p, c->n_stream);
+    c->windowed_last = false;
+    Resolver res(*c, c->d_stream.p, c->n_stream, false);
     res.run();
     c->d_last = c->d_stream.p;
     c->n_last = c->n_stream;
@@ -1577,13 +2180,15 @@ int zc_finish(zc_ctx* c) {
 
 int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
   if (!c || (n && !d_data) || ((uintptr_t)d_data & 15)) return ZC_ERR_ARG;
+  if (c->res) return ZC_ERR_STATE;  // a fed stream is open
   return guarded(c, [&] {
     DeviceGuard g(c->device);
     // the stream may have just been written on the legacy default stream
     // (e.g. torch's): order the context's stream after that work
     HCK(hipEventRecord(c->ev_in, nullptr));
     HCK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
-    Resolver res(*c, (const uint8_t*)d_data, n);
+    c->windowed_last = false;
+    Resolver res(*c, (const uint8_t*)d_data, n, false);
     res.run();
     c->d_last = (const uint8_t*)d_data;
     c->n_last = n;
@@ -1593,6 +2198,7 @@ int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
 
 int zc_chunk_host(zc_ctx* c, const void* host, uint64_t n) {
   if (!c || (n && !host)) return ZC_ERR_ARG;
+  if (c->res) return ZC_ERR_STATE;
   return guarded(c, [&] {
     DeviceGuard g(c->device);
     if (c->d_stream.cap < n) {
@@ -1600,11 +2206,12 @@ int zc_chunk_host(zc_ctx* c, const void* host, uint64_t n) {
       c->d_stream.ensure((n + 4095) & ~uint64_t(4095));
     }
     c->n_stream = n;
+    c->windowed_last = false;
     uint8_t* d = c->d_stream.p;
     const uint8_t* h = (const uint8_t*)host;
     // segments land on the copy stream; the scan of each follows on the
     // context's stream as soon as its copy has completed
-    Resolver res(*c, d, n);
+    Resolver res(*c, d, n, false);
     res.begin();
     for (uint64_t off = 0; off < n; off += kHostSegment) {
       const uint64_t len = std::min<uint64_t>(kHostSegment, n - off);
@@ -1613,7 +2220,7 @@ int zc_chunk_host(zc_ctx* c, const void* host, uint64_t n) {
       HCK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
       res.scan_upto(off + len);
     }
-    res.resolve();
+    res.run_final();
     c->d_last = d;
     c->n_last = n;
     c->finished = true;
@@ -1630,19 +2237,40 @@ int zc_get_records(const zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
   return ZC_OK;
 }
 
+int zc_take_records(zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
+  if (!c || (cap && !out)) return ZC_ERR_ARG;
+  const size_t n = std::min(cap, c->nrec_done);
+  if (n) {
+    memcpy(out, c->recs.data(), n * sizeof(zc_record));
+    c->recs.erase(c->recs.begin(), c->recs.begin() + n);
+    c->nrec_done -= n;
+  }
+  if (n_out) *n_out = n;
+  return ZC_OK;
+}
+
 int zc_get_stats(const zc_ctx* c, zc_stats* out) {
   if (!c || !out) return ZC_ERR_ARG;
   *out = c->stats;
+  out->hbm_bytes = ctx_hbm_bytes(*c);
+  out->hist_entries = c->nhist;
+  out->window_bytes = c->win_cap;
   return ZC_OK;
 }
 
 int zc_reset(zc_ctx* c) {
   if (!c) return ZC_ERR_ARG;
+  if (c->res) {
+    (void)hipStreamSynchronize(c->stream);
+    window_close(*c);
+  }
   c->n_stream = 0;
+  c->wbase = c->wend = 0;
   c->finished = false;
   c->d_last = nullptr;
   c->n_last = 0;
   c->recs.clear();
+  c->nrec_done = 0;
   c->err.clear();
   return ZC_OK;
 }
@@ -1650,14 +2278,23 @@ int zc_reset(zc_ctx* c) {
 int zc_forget_stream_chunks(zc_ctx* c) {
   if (!c) return ZC_ERR_ARG;
   return guarded(c, [&] {
+    DeviceGuard g(c->device);
     c->statics.erase(std::remove_if(c->statics.begin(), c->statics.end(),
                                     [](const StaticEntry& e) { return !e.seeded; }),
                      c->statics.end());
+    index_truncate(*c, 0, c->statics.size(), true);
   });
 }
 
 int zc_read_stream(const zc_ctx* c, uint64_t offset, size_t n, void* host_out) {
-  if (!c || (n && !host_out) || offset > c->n_last || n > c->n_last - offset) return ZC_ERR_ARG;
+  if (!c || (n && !host_out)) return ZC_ERR_ARG;
+  if (c->windowed_last) {
+    // the bytes still in the window (the host mirror)
+    if (offset < c->wbase || offset > c->wend || n > c->wend - offset) return ZC_ERR_ARG;
+    if (n) memcpy(host_out, c->hwin.p + (offset - c->wbase), n);
+    return ZC_OK;
+  }
+  if (offset > c->n_last || n > c->n_last - offset) return ZC_ERR_ARG;
   if (!n) return ZC_OK;
   int prev = -1;
   (void)hipGetDevice(&prev);

@@ -554,7 +554,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
                        (uint32_t)(bk[2 * t + 1] >> 32));
   if (ABL & ABL_TE_DIGEST_ONLY) return kDigests / 2;
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
-  const uint32_t base = (uint32_t)wt * po.wcap;
+  const uint32_t base = (uint32_t)(wt - po.wt0) * po.wcap;
   uint32_t tot = 0, excl = 0;
   bool over = wl.n > ZC_WLIST;
   if (!over) {
@@ -734,7 +734,7 @@ __global__ void __launch_bounds__(ZC_WT_BLOCK) zc_scan_tail_kernel(const uint8_t
                                                              unsigned long long* __restrict__ counters) {
   __shared__ uint32_t s_tmp[ZC_WT_BLOCK / 64];
   const uint64_t wt = tile * (ZC_SCAN_TPB / 64) + blockIdx.x;
-  const uint32_t base = (uint32_t)wt * po.wcap;
+  const uint32_t base = (uint32_t)(wt - po.wt0) * po.wcap;
   const uint32_t tot = wave_tile_block(data, n, wt, lo_thr, blk, po.rel, po.g, base, po.wcap, s_tmp);
   if (threadIdx.x == 0) {
     po.base[wt] = base;
@@ -767,6 +767,14 @@ __global__ void __launch_bounds__(ZC_WT_BLOCK) zc_anchor_rescan_kernel(const uin
   }
 }
 
+// After the feed window slid down by `shift` pool entries: the directory
+// entries [0, cnt) that point into the main pool follow their shares
+__global__ void zc_slide_dir_kernel(uint32_t* __restrict__ base, const uint32_t* __restrict__ dcnt, uint32_t cnt,
+                                    uint32_t shift) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cnt && dcnt[i] != ZC_WT_OVERFLOW && !(base[i] & ZC_SIDE_POOL)) base[i] -= shift;
+}
+
 // the anchors of wave-tile wt: entry k at rel[k], g[k], sorted by position
 struct TileAnchors {
   const uint32_t* rel;
@@ -793,32 +801,13 @@ struct EpochClear {
   unsigned long long* counters;
 };
 
-// zc_chunk_meta: thread per grid chunk i of the epoch, start = r_e + i * W:
-// start, visibility time, key, first anchor (offset, gear value, 64-byte
-// fingerprint); the chunk is not yet consumed by a match (dead = 0).  The
-// whole grid also clears the epoch's tables (no separate fills).
-__global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
-                                     const uint64_t* __restrict__ blk, AnchorView av, uint64_t r_e,
-                                     uint32_t nchunks, uint32_t W, uint64_t pw,
-                                     uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
-                                     uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
-                                     uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
-                                     uint32_t* __restrict__ anc_off, EpochClear ec) {
-  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
-  if (ec.tab)
-    for (uint64_t j = gt; j < ec.twords; j += gs) ec.tab[j] = ~0ull;
-  for (uint64_t j = gt; j < ec.gwords; j += gs) ec.gfilt[j] = 0u;
-  if (gt < CNT_LAST) ec.counters[gt] = 0ull;
-  if (gt >= nchunks) return;
-  const uint32_t i = (uint32_t)gt;
-  const uint64_t c = r_e + (uint64_t)i * W;
-  start[i] = c;
-  vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
-  dead[i] = 0;
-  key[i] = pw + rk_acc(data, blk, c, c + W);
-  uint32_t off = ZC_NO_ANCHOR, gv = 0;
-  uint64_t f = 0;
+// The first anchor of chunk [c, c + W) at offset >= ZC_ANCHOR_MIN_OFF: its
+// offset (ZC_NO_ANCHOR: none), gear value and fingerprint
+__device__ __forceinline__ void first_anchor(const uint8_t* __restrict__ data, const AnchorView& av, uint64_t c,
+                                             uint32_t W, uint32_t& off, uint32_t& gv, uint64_t& f) {
+  off = ZC_NO_ANCHOR;
+  gv = 0;
+  f = 0;
   if (W > ZC_ANCHOR_MIN_OFF) {
     const uint64_t lo = c + ZC_ANCHOR_MIN_OFF, hi = c + W - 1;  // inclusive
     for (uint64_t wt = lo >> ZC_WT_SHIFT; wt <= (hi >> ZC_WT_SHIFT); ++wt) {
@@ -860,6 +849,54 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
       }
     }
   }
+}
+
+// zc_chunk_meta: thread per grid chunk i of the epoch, start = r_e + i * W:
+// start, visibility time, key, first anchor (offset, gear value, 64-byte
+// fingerprint); the chunk is not yet consumed by a match (dead = 0).  The
+// whole grid also clears the epoch's tables (no separate fills).
+__global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
+                                     const uint64_t* __restrict__ blk, AnchorView av, uint64_t r_e,
+                                     uint32_t nchunks, uint32_t W, uint64_t pw,
+                                     uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
+                                     uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
+                                     uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
+                                     uint32_t* __restrict__ anc_off, EpochClear ec) {
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
+  if (ec.tab)
+    for (uint64_t j = gt; j < ec.twords; j += gs) ec.tab[j] = ~0ull;
+  for (uint64_t j = gt; j < ec.gwords; j += gs) ec.gfilt[j] = 0u;
+  if (gt < CNT_LAST) ec.counters[gt] = 0ull;
+  if (gt >= nchunks) return;
+  const uint32_t i = (uint32_t)gt;
+  const uint64_t c = r_e + (uint64_t)i * W;
+  start[i] = c;
+  vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
+  dead[i] = 0;
+  key[i] = pw + rk_acc(data, blk, c, c + W);
+  uint32_t off, gv;
+  uint64_t f;
+  first_anchor(data, av, c, W, off, gv, f);
+  anc_off[i] = off;
+  cg[i] = gv;
+  cfp[i] = f;
+}
+
+// zc_ref_meta: thread per chunk [start[i], start[i] + W) anywhere in the
+// resident stream: key, first anchor {offset, gear, fingerprint} (the
+// chunks that join the historic index)
+__global__ void zc_ref_meta_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk, AnchorView av,
+                                   const uint64_t* __restrict__ starts, uint32_t cnt, uint32_t W, uint64_t pw,
+                                   uint64_t* __restrict__ key, uint32_t* __restrict__ anc_off,
+                                   uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt) return;
+  const uint64_t c = starts[i];
+  key[i] = pw + rk_acc(data, blk, c, c + W);
+  uint32_t off, gv;
+  uint64_t f;
+  first_anchor(data, av, c, W, off, gv, f);
   anc_off[i] = off;
   cg[i] = gv;
   cfp[i] = f;
@@ -902,7 +939,7 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
                                              uint64_t r, uint64_t n, uint32_t W,
                                              Cand* __restrict__ cand, uint64_t cand_cap,
                                              unsigned long long* __restrict__ counters) {
-  if (pos < r + ZC_ANCHOR_MIN_OFF) return;
+  if (pos < r + ZC_ANCHOR_MIN_OFF || !tab) return;
   const uint32_t mask = (1u << tbits) - 1;
   uint32_t h = table_slot(gk, tbits);
   // the filter passed, so the gear is almost surely in the table: the
@@ -932,12 +969,47 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
   }
 }
 
+// The historic index (chunks whose bytes have left HBM: earlier streams of
+// the context, or evicted from a bounded feed window) is a second table of the
+// same layout.  Its entries are always visible and never consumed; a
+// candidate names the entry (pad = 1) and is confirmed by the window's key and
+// SHA-1 (chunk_index.cc:119-143), not by bytes.
+__device__ __forceinline__ void probe_hist(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
+                                           const HistTab& ht, uint64_t r, uint64_t n, uint32_t W,
+                                           Cand* __restrict__ cand, uint64_t cand_cap,
+                                           unsigned long long* __restrict__ counters) {
+  if (pos < r + ZC_ANCHOR_MIN_OFF) return;
+  const uint32_t mask = (1u << ht.bits) - 1;
+  uint32_t h = table_slot(gk, ht.bits);
+  const uint64_t fp = anchor_fp(data, pos);
+  for (;;) {
+    const uint4 slot = *(const uint4*)(ht.tab + 2 * (uint64_t)h);
+    if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
+    if (slot.x == gk && fp == (((uint64_t)slot.w << 32) | slot.z)) {
+      const uint32_t e = slot.y;
+      const uint64_t o = ht.anc[e];
+      if (pos >= r + o) {
+        const uint64_t p = pos - o + W - 1;
+        if (p < n) {
+          const unsigned long long c = atomicAdd(&counters[CNT_CAND], 1ull);
+          if (c < cand_cap) {
+            cand[c].p = p;
+            cand[c].ref = e;
+            cand[c].pad = 1;
+          }
+        }
+      }
+    }
+    h = (h + 1) & mask;
+  }
+}
+
 template <int kProbeWT, int kProbeSlots>
 __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const uint8_t* __restrict__ data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* __restrict__ tab,
     uint32_t tbits, const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off,
     const uint32_t* __restrict__ cls, const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r,
-    uint64_t n, uint32_t W,
+    uint64_t n, uint32_t W, HistTab ht,
     Cand* __restrict__ cand, uint64_t cand_cap, unsigned long long* __restrict__ counters) {
   const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
@@ -959,12 +1031,14 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     live[q] = e < ta[t].cnt;
     g[q] = live[q] ? ta[t].g[e] : 0u;
   }
-  // level 2: the filter word of every live slot
+  // level 2: the filter word of every live slot (bit 0: the epoch's table,
+  // bit 1: the historic one)
   uint32_t f[kS];
 #pragma unroll
   for (int q = 0; q < kS; ++q) {
     const uint32_t fb = g[q] & ((1u << kGFiltBits) - 1);
-    f[q] = live[q] ? (gfilt[fb >> 5] >> (fb & 31)) & 1u : 0u;
+    f[q] = live[q] && gfilt ? (gfilt[fb >> 5] >> (fb & 31)) & 1u : 0u;
+    if (ht.tab) f[q] |= live[q] ? ((ht.filt[fb >> 5] >> (fb & 31)) & 1u) << 1 : 0u;
   }
   // level 3: the offsets of the anchors that pass, compacted into the wave's
   // LDS list {offset in the wave pair | wave-tile << 24, gear}
@@ -976,12 +1050,12 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const int t = q / kProbeSlots;
     rel[q] = f[q] ? ta[t].rel[lane + 64u * (q % kProbeSlots)] : 0u;
   }
-  static_assert(ZC_WT_SHIFT < 24 && kProbeWT <= 256, "pass-list packing");
+  static_assert(ZC_WT_SHIFT < 24 && kProbeWT <= 64, "pass-list packing");
   uint32_t np = 0;
 #pragma unroll
   for (int q = 0; q < kS; ++q) {
     const uint64_t m = __ballot(f[q] != 0u);
-    if (f[q]) lst[np + lane_prefix(m)] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24, g[q]);
+    if (f[q]) lst[np + lane_prefix(m)] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24 | f[q] << 30, g[q]);
     np += (uint32_t)__popcll(m);
   }
   __builtin_amdgcn_wave_barrier();
@@ -989,9 +1063,11 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
   // level 4: the table walks, one anchor per lane
   for (uint32_t j = lane; j < np; j += 64) {
     const uint2 a = lst[j];
-    const uint32_t t = a.x >> 24;
-    probe_anchor(data, ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu), a.y, tab, tbits, anc_off,
-                 cls, vis, dead, r, n, W, cand, cand_cap, counters);
+    const uint32_t t = (a.x >> 24) & 63u;
+    const uint64_t pos = ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu);
+    if (a.x & (1u << 30))
+      probe_anchor(data, pos, a.y, tab, tbits, anc_off, cls, vis, dead, r, n, W, cand, cand_cap, counters);
+    if (a.x & (1u << 31)) probe_hist(data, pos, a.y, ht, r, n, W, cand, cand_cap, counters);
   }
   // wave-tiles with more anchors than the slots above
 #pragma unroll
@@ -999,9 +1075,11 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     for (uint32_t e = lane + 64u * kProbeSlots; e < ta[t].cnt; e += 64) {
       const uint32_t gk = ta[t].g[e];
       const uint32_t fb = gk & ((1u << kGFiltBits) - 1);
-      if ((gfilt[fb >> 5] >> (fb & 31)) & 1u)
-        probe_anchor(data, (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e], gk, tab, tbits, anc_off, cls, vis, dead, r, n, W,
-                     cand, cand_cap, counters);
+      const uint64_t pos = (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e];
+      if (gfilt && ((gfilt[fb >> 5] >> (fb & 31)) & 1u))
+        probe_anchor(data, pos, gk, tab, tbits, anc_off, cls, vis, dead, r, n, W, cand, cand_cap, counters);
+      if (ht.tab && ((ht.filt[fb >> 5] >> (fb & 31)) & 1u))
+        probe_hist(data, pos, gk, ht, r, n, W, cand, cand_cap, counters);
     }
   }
 }
@@ -1106,6 +1184,27 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
                                               (unsigned long long)word);
     if (prev == kEmpty) {
       tab[2 * (uint64_t)h + 1] = cfp[i];
+      return;
+    }
+  }
+}
+
+// historic index: entries [e0, e0 + cnt) (each with an anchor) into its
+// table and filter
+__global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint64_t* __restrict__ fp, uint32_t e0,
+                                      uint32_t cnt, uint64_t* tab, uint32_t bits, uint32_t* __restrict__ filt) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= cnt) return;
+  const uint32_t e = e0 + t, gv = g[e];
+  const uint32_t fb = gv & ((1u << kGFiltBits) - 1);
+  atomicOr(&filt[fb >> 5], 1u << (fb & 31));
+  const uint64_t word = ((uint64_t)e << 32) | gv;
+  const uint32_t mask = (1u << bits) - 1;
+  for (uint32_t h = table_slot(gv, bits);; h = (h + 1) & mask) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
+                                              (unsigned long long)word);
+    if (prev == kEmpty) {
+      tab[2 * (uint64_t)h + 1] = fp[e];
       return;
     }
   }
@@ -1939,12 +2038,36 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
 
 uint32_t probe_filter_words() { return kGFiltWords; }
 
+hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView av, const uint64_t* starts,
+                           uint32_t cnt, uint32_t W, uint64_t pw, uint64_t* key, uint32_t* anc_off, uint32_t* cg,
+                           uint64_t* cfp, hipStream_t s) {
+  if (!cnt) return hipSuccess;
+  hipLaunchKernelGGL(zc_ref_meta_kernel, dim3(blocks_for(cnt, 128)), dim3(128), 0, s, data, blk, av, starts, cnt, W, pw,
+                     key, anc_off, cg, cfp);
+  return hipGetLastError();
+}
+
+hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, uint32_t e0, uint32_t cnt, uint64_t* tab,
+                              uint32_t bits, uint32_t* filt, hipStream_t s) {
+  if (!cnt) return hipSuccess;
+  hipLaunchKernelGGL(zc_hist_insert_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, g, fp, e0, cnt, tab, bits,
+                     filt);
+  return hipGetLastError();
+}
+
+hipError_t launch_slide_dir(uint32_t* base, const uint32_t* cnt_arr, uint32_t cnt, uint32_t shift, hipStream_t s) {
+  if (!cnt || !shift) return hipSuccess;
+  hipLaunchKernelGGL(zc_slide_dir_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, base, cnt_arr, cnt, shift);
+  return hipGetLastError();
+}
+
 
 hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
                         uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint32_t* cls,
-                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W, Cand* cand,
-                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
-  if (!nwt) return hipSuccess;
+                        const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W,
+                        const HistTab& ht, Cand* cand, uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
+  if (!nwt || (!tab && !ht.tab)) return hipSuccess;
+  if (!tab) gfilt = nullptr;
   // 4 wave-tiles per wave, 2 slots per lane each (128 anchors per wave-tile
   // before the extra loop; 64 expected at W = 64 KiB): 60 us per 8 GiB vs 68
   // for 2 x 4 and 8 x 2 (the probe is bound by its random reads: ~100 MB of
@@ -1952,7 +2075,7 @@ hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64
   constexpr int kWT = 4, kSlots = 2;
   const uint64_t waves = (nwt + kWT - 1) / kWT;
   hipLaunchKernelGGL((zc_probe_kernel<kWT, kSlots>), dim3(blocks_for(waves * 64, kProbeTPB)), dim3(kProbeTPB), 0, s,
-                     data, av, wt0, nwt, tab, tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, cand, cand_cap,
+                     data, av, wt0, nwt, tab, tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, ht, cand, cand_cap,
                      counters);
   return hipGetLastError();
 }
