@@ -192,9 +192,9 @@ struct HistTab {
   const uint32_t* filt;
   const uint32_t* anc;  // first anchor offset per entry
 };
-// entries [e0, e0 + cnt) of g / fp into the table and its filter
-hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, uint32_t e0, uint32_t cnt, uint64_t* tab,
-                              uint32_t bits, uint32_t* filt, hipStream_t s);
+// entries [e0, e0 + cnt) of g / fp with an anchor (anc) into the table and its filter
+hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, const uint32_t* anc, uint32_t e0, uint32_t cnt,
+                              uint64_t* tab, uint32_t bits, uint32_t* filt, hipStream_t s);
 // after the window slid by `shift` pool entries: directory entries [0, cnt)
 // that point into the main pool are moved down with it
 hipError_t launch_slide_dir(uint32_t* base, const uint32_t* cnt_arr, uint32_t cnt, uint32_t shift, hipStream_t s);

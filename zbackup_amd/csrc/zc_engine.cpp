@@ -43,7 +43,6 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
-#include <unordered_set>
 #include <vector>
 
 #include "../../include/zchunk.h"
@@ -261,20 +260,6 @@ class HostPool {
   bool stop_ = false;
 };
 
-// an index entry known by value: (rolling key, SHA-1 prefix)
-struct IdKey {
-  uint64_t key;
-  uint8_t sha[16];
-  bool operator==(const IdKey& o) const { return key == o.key && memcmp(sha, o.sha, 16) == 0; }
-};
-struct IdKeyHash {
-  size_t operator()(const IdKey& k) const {
-    uint64_t s;
-    memcpy(&s, k.sha, 8);
-    return (size_t)(k.key ^ (s * 0x9E3779B97F4A7C15ull));
-  }
-};
-
 class Resolver;
 
 }  // namespace
@@ -321,7 +306,6 @@ struct zc_ctx {
   DevBuf<uint64_t> hfp, htab;
   DevBuf<uint32_t> hfilt;
   uint32_t hbits = 0;
-  std::unordered_set<IdKey, IdKeyHash> seen;  // every (key, SHA-1) of the two sets above
 
   // records: recs holds those not yet taken (zc_take_records); the first
   // nrec_done of them are complete (digests and chunk ids filled in)
@@ -413,25 +397,17 @@ void hist_table(zc_ctx& c, uint32_t from) {
     HCK(hipMemsetAsync(c.htab.p, 0xFF, (2ull << bits) * sizeof(uint64_t), c.stream));
     HCK(hipMemsetAsync(c.hfilt.p, 0, probe_filter_words() * sizeof(uint32_t), c.stream));
   }
-  HCK(launch_hist_insert(c.hg.p, c.hfp.p, from, c.nhist - from, c.htab.p, c.hbits, c.hfilt.p, c.stream));
+  HCK(launch_hist_insert(c.hg.p, c.hfp.p, c.hanc.p, from, c.nhist - from, c.htab.p, c.hbits, c.hfilt.p, c.stream));
 }
 
-// append entries (their key and SHA-1 already in hkey / hsha) to the device
-// arrays and the table
-void hist_append(zc_ctx& c, const std::vector<uint32_t>& g, const std::vector<uint32_t>& anc,
-                 const std::vector<uint64_t>& fp) {
-  const uint32_t k = (uint32_t)g.size();
-  if (!k) return;
-  c.hg.grow_keep(c.nhist + k, c.nhist, c.stream);
-  c.hanc.grow_keep(c.nhist + k, c.nhist, c.stream);
-  c.hfp.grow_keep(c.nhist + k, c.nhist, c.stream);
-  h2d(c, c.hg.p + c.nhist, g.data(), k);
-  h2d(c, c.hanc.p + c.nhist, anc.data(), k);
-  h2d(c, c.hfp.p + c.nhist, fp.data(), k);
-  const uint32_t from = c.nhist;
-  c.nhist += k;
-  hist_table(c, from);
-  sync(c);  // the host vectors may go away
+// a by-value entry unless (key, SHA-1) is indexed already (registerNewChunkId,
+// chunk_index.cc:163-182)
+void add_static_once(zc_ctx& c, uint64_t key, const uint8_t* sha, uint8_t seeded) {
+  auto it = c.smap.find(key);
+  if (it != c.smap.end())
+    for (uint32_t i : it->second)
+      if (memcmp(c.statics[i].sha, sha, 16) == 0) return;
+  add_static(c, key, sha, seeded);
 }
 
 // keep the first nh historic entries and the first ns by-value entries
@@ -442,20 +418,7 @@ void index_truncate(zc_ctx& c, uint32_t nh, size_t ns, bool force = false) {
   c.hsha.resize(16 * (size_t)c.nhist);
   if (ns < c.statics.size()) c.statics.resize(ns);
   c.smap.clear();
-  c.seen.clear();
-  for (uint32_t i = 0; i < c.statics.size(); ++i) {
-    c.smap[c.statics[i].key].push_back(i);
-    IdKey id;
-    id.key = c.statics[i].key;
-    memcpy(id.sha, c.statics[i].sha, 16);
-    c.seen.insert(id);
-  }
-  for (uint32_t i = 0; i < c.nhist; ++i) {
-    IdKey id;
-    id.key = c.hkey[i];
-    memcpy(id.sha, &c.hsha[16 * (size_t)i], 16);
-    c.seen.insert(id);
-  }
+  for (uint32_t i = 0; i < c.statics.size(); ++i) c.smap[c.statics[i].key].push_back(i);
   c.hbits = 0;  // rebuilt
   hist_table(c, 0);
 }
@@ -632,22 +595,23 @@ class Resolver {
   uint64_t chk_wt() const { return chk_wt_; }  // wave-tiles below have been checked
 
   // New index entries from this context's chunks [starts[i], starts[i] + W)
-  // (resident): those with an anchor join the historic table, those without
-  // the by-value set of the exact screen; (key, SHA-1) pairs already indexed
-  // are skipped, as registerNewChunkId does (chunk_index.cc:163-182).
+  // (resident): all of them join the historic index (key and SHA-1 on the
+  // host, first anchor on the device; those with an anchor enter its table),
+  // those without an anchor also the by-value set of the exact screen.
   // sha16: the chunks' SHA-1 prefixes when known (16 bytes each), else
   // computed here.
   void hist_add(const std::vector<uint64_t>& starts, const uint8_t* sha16) {
     const uint32_t k = (uint32_t)starts.size();
     if (!k || !indexable_) return;
+    const uint32_t e0 = c_.nhist;
     c_.va.ensure(k);
+    c_.hanc.grow_keep(e0 + k, e0, c_.stream);
+    c_.hg.grow_keep(e0 + k, e0, c_.stream);
+    c_.hfp.grow_keep(e0 + k, e0, c_.stream);
     c_.hm_key.ensure(k);
-    c_.hm_fp.ensure(k);
-    c_.hm_anc.ensure(k);
-    c_.hm_g.ensure(k);
     h2d(c_, c_.va.p, starts.data(), k);
-    HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, k, W_, pow257(W_), c_.hm_key.p, c_.hm_anc.p, c_.hm_g.p,
-                        c_.hm_fp.p, c_.stream));
+    HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, k, W_, pow257(W_), c_.hm_key.p, c_.hanc.p + e0, c_.hg.p + e0,
+                        c_.hfp.p + e0, c_.stream));
     std::vector<uint8_t> sha20;
     if (!sha16) {
       std::vector<uint32_t> len(k, W_);
@@ -658,31 +622,22 @@ class Resolver {
       sha20.resize((size_t)k * 20);
       d2h(c_, sha20.data(), c_.sha_out.p, sha20.size());
     }
-    std::vector<uint64_t> key(k), fp(k);
-    std::vector<uint32_t> anc(k), g(k);
-    d2h(c_, key.data(), c_.hm_key.p, k);
-    d2h(c_, fp.data(), c_.hm_fp.p, k);
-    d2h(c_, anc.data(), c_.hm_anc.p, k);
-    d2h(c_, g.data(), c_.hm_g.p, k);
+    c_.hkey.resize((size_t)e0 + k);
+    std::vector<uint32_t> anc(k);
+    d2h(c_, c_.hkey.data() + e0, c_.hm_key.p, k);
+    d2h(c_, anc.data(), c_.hanc.p + e0, k);
     sync(c_);
-    std::vector<uint32_t> ng, nanc;
-    std::vector<uint64_t> nfp;
-    for (uint32_t i = 0; i < k; ++i) {
-      IdKey id;
-      id.key = key[i];
-      memcpy(id.sha, sha16 ? sha16 + 16 * (size_t)i : &sha20[20 * (size_t)i], 16);
-      if (!c_.seen.insert(id).second) continue;
-      if (anc[i] == ZC_NO_ANCHOR) {
-        add_static(c_, id.key, id.sha, 0);
-        continue;
-      }
-      c_.hkey.push_back(id.key);
-      c_.hsha.insert(c_.hsha.end(), id.sha, id.sha + 16);
-      ng.push_back(g[i]);
-      nanc.push_back(anc[i]);
-      nfp.push_back(fp[i]);
+    c_.hsha.resize(16 * ((size_t)e0 + k));
+    uint8_t* hs = c_.hsha.data() + 16 * (size_t)e0;
+    if (sha16) {
+      memcpy(hs, sha16, 16 * (size_t)k);
+    } else {
+      for (uint32_t i = 0; i < k; ++i) memcpy(hs + 16 * (size_t)i, &sha20[20 * (size_t)i], 16);
     }
-    hist_append(c_, ng, nanc, nfp);
+    for (uint32_t i = 0; i < k; ++i)
+      if (anc[i] == ZC_NO_ANCHOR) add_static_once(c_, c_.hkey[e0 + i], hs + 16 * (size_t)i, 0);
+    c_.nhist = e0 + k;
+    hist_table(c_, e0);
   }
 
  private:
@@ -2063,11 +2018,7 @@ int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
   return guarded(c, [&] {
     for (size_t i = 0; i < n; ++i) {
       if (seeds[i].size != c->W) continue;  // only W-byte entries can equal a W-byte window
-      IdKey id;
-      id.key = seeds[i].rolling;
-      memcpy(id.sha, seeds[i].sha1, 16);
-      if (!c->seen.insert(id).second) continue;  // registerNewChunkId: already indexed
-      add_static(*c, id.key, id.sha, 1);
+      add_static_once(*c, seeds[i].rolling, seeds[i].sha1, 1);
     }
   });
 }

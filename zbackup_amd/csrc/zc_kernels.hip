@@ -1189,13 +1189,15 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
   }
 }
 
-// historic index: entries [e0, e0 + cnt) (each with an anchor) into its
-// table and filter
-__global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint64_t* __restrict__ fp, uint32_t e0,
-                                      uint32_t cnt, uint64_t* tab, uint32_t bits, uint32_t* __restrict__ filt) {
+// historic index: entries [e0, e0 + cnt) that have an anchor into its table
+// and filter
+__global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint64_t* __restrict__ fp,
+                                      const uint32_t* __restrict__ anc, uint32_t e0, uint32_t cnt, uint64_t* tab,
+                                      uint32_t bits, uint32_t* __restrict__ filt) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cnt) return;
   const uint32_t e = e0 + t, gv = g[e];
+  if (anc[e] == ZC_NO_ANCHOR) return;
   const uint32_t fb = gv & ((1u << kGFiltBits) - 1);
   atomicOr(&filt[fb >> 5], 1u << (fb & 31));
   const uint64_t word = ((uint64_t)e << 32) | gv;
@@ -2047,11 +2049,11 @@ hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView 
   return hipGetLastError();
 }
 
-hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, uint32_t e0, uint32_t cnt, uint64_t* tab,
-                              uint32_t bits, uint32_t* filt, hipStream_t s) {
+hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, const uint32_t* anc, uint32_t e0, uint32_t cnt,
+                              uint64_t* tab, uint32_t bits, uint32_t* filt, hipStream_t s) {
   if (!cnt) return hipSuccess;
-  hipLaunchKernelGGL(zc_hist_insert_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, g, fp, e0, cnt, tab, bits,
-                     filt);
+  hipLaunchKernelGGL(zc_hist_insert_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, g, fp, anc, e0, cnt, tab,
+                     bits, filt);
   return hipGetLastError();
 }
 
