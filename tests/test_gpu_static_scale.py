@@ -1,0 +1,74 @@
+"""The static index at repository scale: ChunkIndex::loadIndex
+registers every chunk of every index file (chunk_index.cc:26-79) and findChunk
+probes all of them at every byte (chunk_index.cc:119-143).  Ids known only by
+value (no bytes, no anchors) go through the exact screen; past 2048 keys it
+tests a Bloom filter at every position and trims its runs on the device to
+exact 64-bit key hits.  Seeded with 3,000 / 300,000 random ids plus the real
+ids of a block and of the all-zero chunk that the stream contains: records
+bit-exact vs the oracle (device-resident and through the feed window)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+W64 = 65536
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    from zbackup_amd import _build
+    _build.build()
+    oracle.build()
+    return torch
+
+
+def _same(got, want):
+    assert len(got) == len(want), (len(got), len(want))
+    for f in ("offset", "size", "kind", "rolling"):
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert bad.size == 0, f"{f} differs at {bad.size} records, first {bad[:4]}"
+    bad = np.nonzero((got["sha1"] != want["sha1"]).any(axis=1))[0]
+    assert bad.size == 0, f"sha1 differs at {bad.size} records, first {bad[:4]}"
+
+
+def _seeds(nrand):
+    real = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(oracle.gen("R9:8000000"), W64)
+            if k == "N" and s == W64]
+    zero = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(oracle.gen("Z:65536"), W64)]
+    rng = np.random.default_rng(nrand)
+    keys = rng.integers(1, 2**63, nrand, dtype=np.int64)
+    shas = rng.integers(0, 256, (nrand, 16), dtype=np.uint8)
+    rand = [(shas[i].tobytes(), int(keys[i]), W64) for i in range(nrand)]
+    return real + zero + rand, len(real)
+
+
+SPEC = "R5:30000000,R9:8000000,Z:1000000,R6:20000000,C40000000:3000000,R9:3000000"
+
+
+@pytest.mark.parametrize("nrand", [3000, 300000])
+def test_large_static_index_device_vs_oracle(torch_cuda, nrand):
+    from zbackup_amd import BackupCreator
+    seeds, nreal = _seeds(nrand)
+    data = oracle.gen(SPEC)
+    want = oracle.chunk_array(data, W64, seeds=seeds)
+    assert (want["kind"] == 1).sum() >= nreal
+    t = torch_cuda.from_numpy(data).to("cuda")
+    with BackupCreator(W64, seeds=seeds, sha1=True) as bc:
+        bc.chunk_device(t.data_ptr(), data.size)
+        _same(bc.records(), want)
+
+
+def test_large_static_index_window_vs_oracle(torch_cuda):
+    from zbackup_amd import BackupCreator
+    seeds, _ = _seeds(300000)
+    data = oracle.gen(SPEC)
+    want = oracle.chunk_array(data, W64, seeds=seeds)
+    with BackupCreator(W64, seeds=seeds, sha1=True, window=1) as bc:
+        bc.feed(data)
+        bc.finish()
+        _same(bc.records(), want)

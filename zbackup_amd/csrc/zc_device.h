@@ -107,6 +107,30 @@ struct PoolOut {
   uint64_t wt0;
 };
 
+// Blocked Bloom filter of the exact screen's large key sets (more than the
+// LDS holds), over the full 64-bit window keys: 2^bits blocks of two 32-bit
+// words (8 bytes, one gather), a key sets three bits in each word
+inline uint32_t bloom_bits_for(size_t keys) {
+  // a block per two keys up to 512 K keys (300 K keys -> 2 MiB, half an XCD's
+  // L2: ~8e-5 false hits per position, screened out on the device by the
+  // 64-bit run filter), a block per key beyond (1 M keys -> 8 MiB: ~5e-5)
+  uint32_t b = 17;
+  while (b < 24 && ((size_t)(keys > (512u << 10) ? 1 : 2) << b) < keys) ++b;
+  return b;
+}
+__host__ __device__ inline uint32_t bloom_block(uint64_t key, uint32_t bits) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+__host__ __device__ inline uint32_t bloom_seed(uint64_t key) {
+  return (uint32_t)(((key ^ (key >> 31)) * 0xBF58476D1CE4E5B9ull) >> 32);
+}
+__host__ __device__ inline uint32_t bloom_lo(uint32_t g) {
+  return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)) | (1u << ((g >> 10) & 31u));
+}
+__host__ __device__ inline uint32_t bloom_hi(uint32_t g) {
+  return (1u << ((g >> 15) & 31u)) | (1u << ((g >> 20) & 31u)) | (1u << ((g >> 25) & 31u));
+}
+
 struct Run {  // maximal run [start, end) of screen hits of the F scan
   uint64_t start, end;
 };
@@ -225,8 +249,9 @@ hipError_t launch_range_digest_small(const uint8_t* data, uint64_t n, const uint
 // runs[tile_off[t] ...], tile_cnt[t] of them (merged inside the tile)
 hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W,
                         uint32_t pw32, uint64_t p_start, uint64_t p_end, uint64_t tile0, uint64_t ntiles,
-                        const uint32_t* f32, uint32_t nf, const uint32_t* fbits, Run* runs, uint64_t runs_cap,
-                        uint64_t* tile_off, uint32_t* tile_cnt, unsigned long long* counters, hipStream_t s);
+                        const uint32_t* f32, uint32_t nf, const uint32_t* fbits, const uint32_t* bloom,
+                        uint32_t bloom_bits, Run* runs, uint64_t runs_cap, uint64_t* tile_off, uint32_t* tile_cnt,
+                        unsigned long long* counters, hipStream_t s);
 
 // exact screen, staged: screen wave-tiles [wt0, wt0 + nwt) of ZC_FWT bytes,
 // each starting before p_end <= n (W >= 32, n >= 64), positions p in
@@ -241,6 +266,23 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
                                const uint32_t* d_keys32, uint32_t nf, const uint32_t* fbits17, Run* runs,
                                uint64_t runs_cap, uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters,
                                hipStream_t s);
+
+// the large-key-set screen: nf > 2048 keys go through the Bloom filter
+// `bloom` (2^bloom_bits uint2 blocks) of the 64-bit window key, rolled at
+// every position (the staged kernel's runs are then trimmed by key64_filter)
+hipError_t launch_fscan_staged_bloom(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
+                                     uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt,
+                                     const uint32_t* bloom, uint32_t bloom_bits, Run* runs, uint64_t runs_cap, uint64_t* wt_off,
+                                     uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s);
+// set the bits of the 64-bit keys[0, n) in a Bloom filter
+hipError_t launch_bloom_add(uint32_t* bloom, uint32_t bits, const uint64_t* keys, uint32_t n, hipStream_t s);
+// Short screen runs (<= 64 positions) are trimmed to the positions whose
+// exact 64-bit window key is in the sets (a hash set of 2^sbits slots, empty
+// slot = 0, key 0 present iff zero_key; plus nl sorted keys `list`); a run
+// with none becomes empty (start = end).  Longer runs are left as they are.
+hipError_t launch_key64_filter(const uint8_t* data, const uint64_t* blk, uint32_t W, uint64_t pw, Run* runs,
+                               uint64_t nruns, const uint64_t* set, uint32_t sbits, int zero_key,
+                               const uint64_t* list, uint32_t nl, hipStream_t s);
 
 hipError_t launch_sha1(const uint8_t* data, const uint64_t* a, const uint32_t* len, uint32_t nr,
                        uint8_t* out20, hipStream_t s);

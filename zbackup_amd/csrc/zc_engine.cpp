@@ -297,6 +297,16 @@ struct zc_ctx {
   // context's chunks without an anchor; probed by the exact screen
   std::vector<StaticEntry> statics;  // entries of size W
   std::unordered_map<uint64_t, std::vector<uint32_t>> smap;  // key -> statics
+  uint64_t statics_ver = 1;  // bumped when the by-value set changes
+  // the by-value set's screen structures for large sets (built for statics_ver)
+  uint64_t sc_ver = 0;
+  std::vector<uint32_t> sc_fbits;  // zc_fscan's 2^19-bit map
+  DevBuf<uint32_t> bloom_s, bloom_w;  // Bloom filter of the set (and per epoch with the epoch's keys)
+  uint32_t bloom_bits = 0;
+  DevBuf<uint64_t> kset;              // 64-bit keys, open addressing (empty = 0)
+  uint32_t kset_bits = 0;
+  int kset_zero = 0;
+  DevBuf<uint64_t> flist;  // the epoch's anchorless keys, sorted (64-bit)
   // historic index: this context's W-byte chunks whose bytes are gone from HBM
   // (earlier streams, or evicted from the window), each with its first anchor
   std::vector<uint64_t> hkey;
@@ -380,6 +390,45 @@ void add_static(zc_ctx& c, uint64_t key, const uint8_t* sha, uint8_t seeded) {
   e.seeded = seeded;
   c.smap[key].push_back((uint32_t)c.statics.size());
   c.statics.push_back(e);
+  ++c.statics_ver;
+}
+
+// the large-set screen structures of the by-value set, rebuilt when it changed
+void statics_screen(zc_ctx& c) {
+  if (c.sc_ver == c.statics_ver) return;
+  std::vector<uint64_t> keys;
+  keys.reserve(c.smap.size());
+  for (const auto& kv : c.smap) keys.push_back(kv.first);
+  c.sc_fbits.assign(1u << 14, 0);
+  c.bloom_bits = bloom_bits_for(keys.size() + 64);
+  std::vector<uint32_t> bloom(2u << c.bloom_bits, 0);
+  uint32_t bits = 10;
+  while ((1ull << bits) < 2ull * keys.size() + 2) ++bits;
+  std::vector<uint64_t> set(1ull << bits, 0);
+  c.kset_zero = 0;
+  for (uint64_t k : keys) {
+    const uint32_t h = (uint32_t)k;
+    c.sc_fbits[h >> 18] |= 1u << ((h >> 13) & 31);
+    const uint32_t b = bloom_block(k, c.bloom_bits), g = bloom_seed(k);
+    bloom[2 * b] |= bloom_lo(g);
+    bloom[2 * b + 1] |= bloom_hi(g);
+    if (k == 0) {
+      c.kset_zero = 1;
+      continue;
+    }
+    for (uint64_t s = (k * 0x9E3779B97F4A7C15ull) >> (64 - bits);; s = (s + 1) & ((1ull << bits) - 1))
+      if (set[s] == 0) {
+        set[s] = k;
+        break;
+      }
+  }
+  c.bloom_s.ensure(bloom.size());
+  c.kset.ensure(set.size());
+  c.kset_bits = bits;
+  h2d(c, c.bloom_s.p, bloom.data(), bloom.size());
+  h2d(c, c.kset.p, set.data(), set.size());
+  sync(c);
+  c.sc_ver = c.statics_ver;
 }
 
 // historic table: 2^hbits >= 2 nhist slots; grows by a rebuild, otherwise
@@ -419,6 +468,7 @@ void index_truncate(zc_ctx& c, uint32_t nh, size_t ns, bool force = false) {
   if (ns < c.statics.size()) c.statics.resize(ns);
   c.smap.clear();
   for (uint32_t i = 0; i < c.statics.size(); ++i) c.smap[c.statics[i].key].push_back(i);
+  ++c.statics_ver;
   c.hbits = 0;  // rebuilt
   hist_table(c, 0);
 }
@@ -743,6 +793,7 @@ class Resolver {
   uint64_t fmemo_key_ = 0;
   bool fmemo_valid_ = false;
   std::vector<Run> runs_;
+  uint32_t flist_n_ = 0;
   uint64_t f_min_vis_ = kInf;
   bool has_f_ = false;
 
@@ -1191,17 +1242,45 @@ class Resolver {
   }
 
   // ---------------------------------------------------------------- F screen
+  // Key sets beyond the LDS (kLdsKeys) take the Bloom mode: the staged
+  // screen tests a 4 MiB Bloom filter in L2 at every position, and its runs
+  // are trimmed on the device to positions whose exact 64-bit key is in the
+  // set before they come back (the filter's false hits never reach the walk)
+  static constexpr size_t kLdsKeys = 2048;
   void fscan() {
     std::vector<uint32_t> keys32;
     for (auto& kv : fmap_) keys32.push_back((uint32_t)kv.first);
-    for (auto& kv : c_.smap) keys32.push_back((uint32_t)kv.first);
+    const bool bloom = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN) &&
+                       c_.smap.size() + fmap_.size() > kLdsKeys;
+    if (!bloom)
+      for (auto& kv : c_.smap) keys32.push_back((uint32_t)kv.first);
     std::sort(keys32.begin(), keys32.end());
     keys32.erase(std::unique(keys32.begin(), keys32.end()), keys32.end());
-    const uint32_t nf = (uint32_t)keys32.size();
-    c_.f32.ensure(std::max<uint32_t>(nf, 1));
-    h2d(c_, c_.f32.p, keys32.data(), nf);
+    const uint32_t nf = bloom ? (uint32_t)(c_.smap.size() + keys32.size()) : (uint32_t)keys32.size();
+    c_.f32.ensure(std::max<size_t>(keys32.size(), 1));
+    h2d(c_, c_.f32.p, keys32.data(), keys32.size());
     c_.fbits.ensure(1u << 14);
-    if (nf > 16) {
+    const uint32_t* bloom_p = nullptr;
+    if (bloom) {
+      statics_screen(c_);
+      std::vector<uint32_t> bits = c_.sc_fbits;
+      for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
+      h2d(c_, c_.fbits.p, bits.data(), bits.size());
+      bloom_p = c_.bloom_s.p;
+      std::vector<uint64_t> fk;
+      for (auto& kv : fmap_) fk.push_back(kv.first);
+      std::sort(fk.begin(), fk.end());
+      c_.flist.ensure(std::max<size_t>(fk.size(), 1));
+      h2d(c_, c_.flist.p, fk.data(), fk.size());
+      flist_n_ = (uint32_t)fk.size();
+      if (!fk.empty()) {  // the epoch's keys join a copy of the set's filter
+        c_.bloom_w.ensure(2u << c_.bloom_bits);
+        HCK(hipMemcpyAsync(c_.bloom_w.p, c_.bloom_s.p, (2 * sizeof(uint32_t)) << c_.bloom_bits,
+                           hipMemcpyDeviceToDevice, c_.stream));
+        HCK(launch_bloom_add(c_.bloom_w.p, c_.bloom_bits, c_.flist.p, (uint32_t)fk.size(), c_.stream));
+        bloom_p = c_.bloom_w.p;
+      }
+    } else if (nf > 16) {
       std::vector<uint32_t> bits(1u << 14, 0);
       for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
       h2d(c_, c_.fbits.p, bits.data(), bits.size());
@@ -1241,21 +1320,26 @@ class Resolver {
       t1 = std::min(t1, ntiles);
       if (t1 > t0)
         HCK(launch_fscan(d_, n_, blk_v(), W_, pw32, p_start, p_end, t0, t1 - t0, c_.f32.p, nf, c_.fbits.p,
-                         c_.runs.p, c_.runs.cap, ftile_off_v, ftile_cnt_v, c_.counters.p, c_.stream));
+                         bloom_p, c_.bloom_bits, c_.runs.p, c_.runs.cap, ftile_off_v, ftile_cnt_v, c_.counters.p, c_.stream));
     };
     std::vector<uint32_t> wcnt(wt_hi - wt_lo);
     for (int attempt = 0; attempt < 3; ++attempt) {
       c_.runs.ensure(cap);
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
-      if (staged) {
+      if (staged && bloom) {
+        HCK(launch_fscan_staged_bloom(d_, n_, blk_v(), W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, bloom_p,
+                                      c_.bloom_bits, c_.runs.p, c_.runs.cap, fwt_off_v, fwt_cnt_v, c_.counters.p, c_.stream));
+      } else if (staged) {
         HCK(launch_fscan_staged(d_, n_, blk_v(), W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(),
                                 c_.f32.p, nf, c_.fbits17.p, c_.runs.p, c_.runs.cap, fwt_off_v, fwt_cnt_v,
                                 c_.counters.p, c_.stream));
+      }
+      if (staged) {
         d2h(c_, wcnt.data(), fwt_cnt_v + wt_lo, wcnt.size());
         sync(c_);
         // wave-tiles whose runs overflowed the lane slots: redo with zc_fscan,
         // one launch per stretch of consecutive ones; a launch costs about the
-        // same for any number of tiles (a lane walks 1 KiB), so past a few
+        // same for any number of tiles (a lane walks 1 KiB), so past 64
         // stretches everything from the first to the last overflowed
         // wave-tile is redone in one launch
         std::vector<std::pair<uint64_t, uint64_t>> st;
@@ -1269,7 +1353,7 @@ class Resolver {
           st.push_back({i, j});
           i = j;
         }
-        if (st.size() > 4) {
+        if (st.size() > 64) {
           for (uint64_t i = st.front().first; i < st.back().second; ++i) wcnt[i] = ZC_FWT_OVERFLOW;
           st = {{st.front().first, st.back().second}};
         }
@@ -1285,6 +1369,9 @@ class Resolver {
     }
     const uint64_t nruns = cnt[CNT_RUNS];
     c_.stats.fscan_runs += nruns;
+    if (bloom)
+      HCK(launch_key64_filter(d_, blk_v(), W_, pow257(W_), c_.runs.p, nruns, c_.kset.p, c_.kset_bits, c_.kset_zero,
+                              c_.flist.p, flist_n_, c_.stream));
     // zc_fscan's per-tile lists are read only where it ran
     bool old_ran = !staged;
     for (uint32_t c : wcnt) old_ran |= c == ZC_FWT_OVERFLOW;
@@ -1300,6 +1387,7 @@ class Resolver {
     sync(c_);
     auto take = [&](const Run* q, uint64_t k) {
       for (uint64_t i = 0; i < k; ++i) {
+        if (q[i].end <= q[i].start) continue;  // emptied by the 64-bit filter
         if (!runs_.empty() && runs_.back().end == q[i].start)
           runs_.back().end = q[i].end;
         else

@@ -1281,7 +1281,10 @@ __global__ void zc_range_digest_small_kernel(const uint8_t* __restrict__ data, u
 // zc_fscan: exact window hash H(p) mod 2^32 at every p >= p_start, screened
 // against the low words of keys without anchors; emits maximal hit runs.
 __device__ __forceinline__ bool f_member(uint32_t h, const uint32_t* f32, uint32_t nf,
-                                         const uint32_t* s_bits) {
+                                         const uint32_t* s_bits, const uint32_t* bloom = nullptr,
+                                         uint32_t bbits = 0) {
+  (void)bloom;
+  (void)bbits;  // (the Bloom mode tests 64-bit keys: zc_fscan_kernel's fhit)
   if (s_bits) return (s_bits[h >> 18] >> ((h >> 13) & 31)) & 1u;  // bit index h >> 13
   bool m = false;
   for (uint32_t k = 0; k < nf; ++k) m |= (f32[k] == h);
@@ -1294,8 +1297,8 @@ constexpr uint32_t kFBitmapWords = 1u << 14;  // 2^19 bits = 64 KiB, index = h >
 __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, const uint64_t* __restrict__ blk, uint32_t W,
     uint32_t pw32, uint64_t p_start, uint64_t p_end, uint64_t tile0, const uint32_t* __restrict__ f32, uint32_t nf,
-    const uint32_t* __restrict__ fbits, Run* __restrict__ runs, uint64_t runs_cap,
-    uint64_t* __restrict__ tile_off, uint32_t* __restrict__ tile_cnt,
+    const uint32_t* __restrict__ fbits, const uint32_t* __restrict__ bloom, uint32_t bbits, Run* __restrict__ runs,
+    uint64_t runs_cap, uint64_t* __restrict__ tile_off, uint32_t* __restrict__ tile_cnt,
     unsigned long long* __restrict__ counters) {
   extern __shared__ uint32_t s_dyn[];  // bitmap (if used)
   __shared__ uint64_t s_rs[ZC_RUN_SLOTS * ZC_TPB], s_re[ZC_RUN_SLOTS * ZC_TPB];
@@ -1320,6 +1323,24 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
   uint64_t pe = span0 + ZC_SPAN < lim ? span0 + ZC_SPAN : lim;
   uint32_t cnt = 0;
   uint64_t open = ~0ull;
+  // the window value: its accumulator mod 2^32 against the key words, or
+  // (Bloom mode, large key sets) mod 2^64 against the 64-bit Bloom filter
+  const uint64_t pw64 = bloom ? pow257_dev(W) : 0;
+  auto fstart = [&](uint64_t a, uint64_t b) -> uint64_t {
+    return bloom ? rk_acc(data, blk, a, b) : (uint64_t)rk_acc32(data, blk, a, b);
+  };
+  auto fstep = [&](uint64_t v, uint32_t bi, uint32_t bo) -> uint64_t {
+    return bloom ? v * 257u + bi - (uint64_t)bo * pw64 : (uint64_t)((uint32_t)v * 257u + bi - bo * pw32);
+  };
+  auto fhit = [&](uint64_t v) -> bool {
+    if (bloom) {
+      const uint64_t key = v + pw64;
+      const uint2 w = ((const uint2*)bloom)[bloom_block(key, bbits)];
+      const uint32_t g = bloom_seed(key), ml = bloom_lo(g), mh = bloom_hi(g);
+      return (w.x & ml) == ml && (w.y & mh) == mh;
+    }
+    return f_member((uint32_t)v + pw32, s_keys, nf, s_bits);
+  };
   auto emit = [&](uint64_t a, uint64_t b) {
     if (cnt < ZC_RUN_SLOTS) {
       s_rs[cnt * ZC_TPB + tid] = a;
@@ -1328,17 +1349,16 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
     ++cnt;
   };
   if (ps < pe) {
-    // window [p-W+1, p] ends at p; V = its accumulator mod 2^32
-    uint32_t V = rk_acc32(data, blk, ps + 1 - W, ps + 1);
-    uint32_t h = V + pw32;
-    if (f_member(h, s_keys, nf, s_bits)) open = ps;
+    // window [p-W+1, p] ends at p
+    uint64_t V = fstart(ps + 1 - W, ps + 1);
+    if (fhit(V)) open = ps;
     uint64_t p = ps + 1;
     for (; p + 4 <= pe; p += 4) {
       uint32_t xin = load4_any(data, p), xout = load4_any(data, p - W);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        V = V * 257u + ((xin >> (8 * k)) & 0xFFu) - ((xout >> (8 * k)) & 0xFFu) * pw32;
-        bool hit = f_member(V + pw32, s_keys, nf, s_bits);
+        V = fstep(V, (xin >> (8 * k)) & 0xFFu, (xout >> (8 * k)) & 0xFFu);
+        bool hit = fhit(V);
         if (hit && open == ~0ull) open = p + k;
         if (!hit && open != ~0ull) {
           emit(open, p + k);
@@ -1347,8 +1367,8 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
       }
     }
     for (; p < pe; ++p) {
-      V = V * 257u + data[p] - (uint32_t)data[p - W] * pw32;
-      bool hit = f_member(V + pw32, s_keys, nf, s_bits);
+      V = fstep(V, data[p], data[p - W]);
+      bool hit = fhit(V);
       if (hit && open == ~0ull) open = p;
       if (!hit && open != ~0ull) {
         emit(open, p);
@@ -1406,12 +1426,12 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
       return;
     }
     // rescan this lane's positions, writing every run
-    uint32_t V = rk_acc32(data, blk, ps + 1 - W, ps + 1);
-    uint64_t o2 = f_member(V + pw32, s_keys, nf, s_bits) ? ps : ~0ull;
+    uint64_t V = fstart(ps + 1 - W, ps + 1);
+    uint64_t o2 = fhit(V) ? ps : ~0ull;
     uint32_t w = 0;
     for (uint64_t p = ps + 1; p < pe; ++p) {
-      V = V * 257u + data[p] - (uint32_t)data[p - W] * pw32;
-      bool hit = f_member(V + pw32, s_keys, nf, s_bits);
+      V = fstep(V, data[p], data[p - W]);
+      bool hit = fhit(V);
       if (hit && o2 == ~0ull) o2 = p;
       if (!hit && o2 != ~0ull) {
         dst[w++] = Run{o2, p};
@@ -1490,8 +1510,24 @@ __host__ __device__ constexpr uint32_t frow_swizzle(uint32_t row) { return (row 
 struct FKeys {
   uint32_t k[16];         // keys - 257^W (compared with V); unused slots repeat k[0]
   const uint32_t* dkeys;  // NF = 32: the nk keys, sorted (copied to LDS)
-  uint32_t nk;
+  uint32_t nk;            // NF = 64: the Bloom filter's size, log2 blocks
+  const uint32_t* bloom;  // NF = 64: the Bloom filter (global memory, L2 resident)
+  uint64_t pw64;          // NF = 64: 257^W mod 2^64
 };
+// run slots per lane per wave-tile: the Bloom mode's false hits (~K / 6e9
+// per position) need more than the exact modes' two
+template <int NF>
+constexpr int kFRS = NF == 64 ? 7 : kFRunSlots;
+
+template <int RS>
+__device__ __forceinline__ void put_run(uint32_t (&rs)[RS], uint32_t (&re)[RS], uint32_t i, uint32_t a, uint32_t b) {
+#pragma unroll
+  for (int k = 0; k < RS; ++k)
+    if (i == (uint32_t)k) {
+      rs[k] = a;
+      re[k] = b;
+    }
+}
 constexpr uint32_t kFLdsKeys = 2048;  // NF = 32: keys searched in LDS (the rest of the 160 KiB)
 
 // Rabin-Karp accumulator mod 2^32 of [a, a + W) for a, W multiples of ZC_SPAN:
@@ -1566,7 +1602,8 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves][2][2 * kSlot];  // [slot][in | out]
   __shared__ uint32_t s_map[NF == 0 || NF == 16 || NF == 32 ? kFMapWords : 1];
   __shared__ uint32_t s_keys[NF == 32 ? kFLdsKeys : 1];
-  __shared__ uint32_t s_rs[kWaves][64 * kFRunSlots], s_re[kWaves][64 * kFRunSlots];
+  constexpr int RS = kFRS<NF>;
+  __shared__ uint32_t s_rs[kWaves][64 * RS], s_re[kWaves][64 * RS];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (NF == 0 || NF == 16 || NF == 32) {
     for (uint32_t i = tid; i < kFMapWords; i += ZC_FTPB) s_map[i] = fmap[i];
@@ -1614,22 +1651,27 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
 #pragma unroll
     for (int j = 0; j < kFDmaHalf; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void_t*)(dst + j * 1024), 16, (int)lane_off[j], 0, 0, 0);
+    // the out-bytes are the in-bytes another lane read a moment ago (W
+    // earlier); their last use: in the Bloom mode marked non-temporal (nt),
+    // so the streamed lines leave L2 to the filter
+    constexpr int kOutAux = NF == 64 ? 2 : 0;
 #pragma unroll
     for (int j = 0; j < kFDmaHalf; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rout, (lds_void_t*)(dst + kSlot + j * 1024), 16,
-                                               (int)(lane_off[j] + oadj), 0, 0, 0);
+                                               (int)(lane_off[j] + oadj), 0, 0, kOutAux);
   };
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
 
   uint32_t V = 0;
+  uint64_t V64 = 0;  // NF = 64: the 64-bit window accumulator
   uint4 carry = make_uint4(0, 0, 0, 0);
   uint64_t wtbase = 0, ps = 0;
   bool open = false, ovf = false;
   uint64_t open_mask = 0;  // wave-uniform mirror of `open`
   bool need_valid = false, head = false;
   uint32_t rstart = 0, nrun = 0;
-  uint32_t rs[kFRunSlots], re[kFRunSlots];
+  uint32_t rs[RS], re[RS];
 
 #pragma unroll 1
   for (uint32_t R = 0; R < nR; ++R) {
@@ -1660,6 +1702,7 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
           carry = make_uint4(w[0], w[1], w[2], w[3]);
         }
       }
+      if constexpr (NF == 64) V64 = ps < n ? rk_acc(data, blk, ps >= W ? ps - W : 0, ps) : 0;
       head = wtbase < (uint64_t)W + 16;
       need_valid = wtbase < p_start || wtbase + ZC_FWT > p_end;
       open = false;
@@ -1679,6 +1722,101 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
       vst[p] = *(const uint4*)(slot + kSlot + lane * ZC_FROUND + ((p ^ sw) << 4));
     }
     wait_lgkmcnt<0>();  // the slot is free
+    if constexpr (NF == 64) {
+      // Bloom mode: the window values of the whole round first, then one
+      // gather of a filter word per position, all in flight together and
+      // issued before the next round's DMA (a later load could not be waited
+      // for without draining that DMA); the per-piece pass below then reads
+      // hit masks
+      uint32_t xo[kFPieces][4], hm[kFPieces];
+#pragma unroll
+      for (int p = 0; p < kFPieces; ++p) {
+        const uint64_t pp = ps + (uint64_t)r * ZC_FROUND + 16 * p;
+        const uint4 vout = funnel16<Q>(p == 0 ? carry : vst[p - 1], vst[p], sbyte);
+        xo[p][0] = vout.x;
+        xo[p][1] = vout.y;
+        xo[p][2] = vout.z;
+        xo[p][3] = vout.w;
+        if (head && pp < W) {
+          const uint64_t z = (uint64_t)W - pp;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const uint64_t lo = 4 * d;
+            xo[p][d] = z >= lo + 4 ? 0u : (z > lo ? xo[p][d] & (~0u << (8 * (z - lo))) : xo[p][d]);
+          }
+        }
+      }
+      // two halves of two pieces: 32 gathers in flight per lane each
+      const uint2* const bl = (const uint2*)K.bloom;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        uint2 bw[2][16];
+        uint32_t gs[2][16];
+#pragma unroll
+        for (int pi = 0; pi < 2; ++pi) {
+          const int p = 2 * hf + pi;
+          const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xo[p][d] >> (8 * q)) & 0xFFu) * K.pw64;
+              const uint64_t key = V64 + K.pw64;
+              bw[pi][4 * d + q] = bl[bloom_block(key, K.nk)];
+              gs[pi][4 * d + q] = bloom_seed(key);
+            }
+        }
+#pragma unroll
+        for (int pi = 0; pi < 2; ++pi) {
+          uint32_t m16 = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const uint32_t ml = bloom_lo(gs[pi][i]), mh = bloom_hi(gs[pi][i]);
+            m16 |= ((bw[pi][i].x & ml) == ml && (bw[pi][i].y & mh) == mh ? 1u : 0u) << i;
+          }
+          hm[2 * hf + pi] = m16;
+        }
+      }
+      if (R + 2 < nR) issue(R + 2);
+#pragma unroll
+      for (int p = 0; p < kFPieces; ++p) {
+        const uint64_t pp = ps + (uint64_t)r * ZC_FROUND + 16 * p;
+        const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
+        uint64_t any = 0, all = ~0ull;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint64_t b = __ballot((hm[p] >> i) & 1u);
+          any |= b;
+          all &= b;
+        }
+        uint64_t need = (open_mask & ~all) | (~open_mask & any);
+        if (need_valid) {
+          const uint64_t some = __ballot(pp < p_start || pp + 16 > p_end);
+          need = (need & ~some) | (some & (any | open_mask));
+        }
+        if (__builtin_expect(need != 0, 0)) {
+          if ((need >> lane) & 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const uint64_t pos = pp + i;
+              const bool h = ((hm[p] >> i) & 1u) && pos >= p_start && pos < p_end;
+              const uint32_t rel = (uint32_t)(pos - wtbase);
+              if (h && !open) {
+                open = true;
+                rstart = rel;
+              } else if (!h && open) {
+                open = false;
+                if (nrun < RS) put_run(rs, re, nrun, rstart, rel);
+                else ovf = true;
+                ++nrun;
+              }
+            }
+          }
+          open_mask = __ballot(open);
+        }
+        (void)xin;
+      }
+    } else {
     if (R + 2 < nR) issue(R + 2);
 
 #pragma unroll
@@ -1730,12 +1868,8 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
                 rstart = rel;
               } else if (!h && open) {
                 open = false;
-                if (nrun < kFRunSlots) {
-                  rs[nrun == 0 ? 0 : 1] = rstart;
-                  re[nrun == 0 ? 0 : 1] = rel;
-                } else {
-                  ovf = true;
-                }
+                if (nrun < RS) put_run(rs, re, nrun, rstart, rel);
+                else ovf = true;
                 ++nrun;
               }
             }
@@ -1743,17 +1877,14 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
         open_mask = __ballot(open);
       }
     }
+    }
     carry = vst[kFPieces - 1];
 
     if (r == kFRounds - 1) {
       // wave-tile end: close runs at span ends, merge across lanes, write
       if (open) {
-        if (nrun < kFRunSlots) {
-          rs[nrun == 0 ? 0 : 1] = rstart;
-          re[nrun == 0 ? 0 : 1] = (lane + 1) * ZC_FLSPAN;
-        } else {
-          ovf = true;
-        }
+        if (nrun < RS) put_run(rs, re, nrun, rstart, (lane + 1) * ZC_FLSPAN);
+        else ovf = true;
         ++nrun;
         open = false;
       }
@@ -1774,19 +1905,25 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
         }
         continue;
       }
-      for (uint32_t i = 0; i < nrun; ++i) {
-        lrs[excl + i] = rs[i == 0 ? 0 : 1];
-        lre[excl + i] = re[i == 0 ? 0 : 1];
-      }
+#pragma unroll
+      for (int k = 0; k < RS; ++k)
+        if ((uint32_t)k < nrun) {
+          lrs[excl + k] = rs[k];
+          lre[excl + k] = re[k];
+        }
       wait_lgkmcnt<0>();
       __builtin_amdgcn_wave_barrier();
       // entry i is a head unless it starts where entry i - 1 ends; lane owns
-      // entries lane and lane + 64 (tot <= 128)
-      const uint32_t i0 = lane, i1 = lane + 64;
-      const bool h0 = i0 < tot && (i0 == 0 || lre[i0 - 1] != lrs[i0]);
-      const bool h1 = i1 < tot && lre[i1 - 1] != lrs[i1];
-      const uint64_t hm0 = __ballot(h0), hm1 = __ballot(h1);
-      const uint32_t nh0 = (uint32_t)__popcll(hm0), nheads = nh0 + (uint32_t)__popcll(hm1);
+      // entries lane + 64 j (tot <= 64 RS)
+      uint64_t hmk[RS];
+      uint32_t nheads = 0;
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const uint32_t i = lane + 64u * j;
+        const bool h = i < tot && (i == 0 || lre[i - 1] != lrs[i]);
+        hmk[j] = __ballot(h);
+        nheads += (uint32_t)__popcll(hmk[j]);
+      }
       uint64_t base = 0;
       if (lane == 0) base = atomicAdd(&counters[CNT_RUNS], (unsigned long long)nheads);
       base = __shfl(base, 0, 64);
@@ -1797,17 +1934,84 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
       }
       if (base + nheads > runs_cap) continue;
       // group index of entry i = heads at or before i, minus one
-      const uint32_t g0 = lane_prefix(hm0) + (h0 ? 1u : 0u) - 1u;
-      const uint32_t g1 = nh0 + lane_prefix(hm1) + (h1 ? 1u : 0u) - 1u;
-      if (i0 < tot) {
-        if (h0) runs[base + g0].start = wtbase + lrs[i0];
-        if (i0 + 1 == tot || lre[i0] != lrs[i0 + 1]) runs[base + g0].end = wtbase + lre[i0];
-      }
-      if (i1 < tot) {
-        if (h1) runs[base + g1].start = wtbase + lrs[i1];
-        if (i1 + 1 == tot || lre[i1] != lrs[i1 + 1]) runs[base + g1].end = wtbase + lre[i1];
+      uint32_t before = 0;
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const uint32_t i = lane + 64u * j;
+        const bool h = (hmk[j] >> lane) & 1;
+        const uint32_t g = before + lane_prefix(hmk[j]) + (h ? 1u : 0u) - 1u;
+        if (i < tot) {
+          if (h) runs[base + g].start = wtbase + lrs[i];
+          if (i + 1 == tot || lre[i] != lrs[i + 1]) runs[base + g].end = wtbase + lre[i];
+        }
+        before += (uint32_t)__popcll(hmk[j]);
       }
     }
+  }
+}
+
+// Bloom filter of a key set (thread per key)
+__global__ void zc_bloom_add_kernel(uint32_t* __restrict__ bloom, uint32_t bits, const uint64_t* __restrict__ keys,
+                                    uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t b = bloom_block(keys[i], bits), g = bloom_seed(keys[i]);
+  atomicOr(&bloom[2 * b], bloom_lo(g));
+  atomicOr(&bloom[2 * b + 1], bloom_hi(g));
+}
+
+// 64-bit key sets of the screen's run filter: open addressing (empty = 0),
+// and a short sorted list
+__device__ __forceinline__ bool key64_in(uint64_t k, const uint64_t* __restrict__ set, uint32_t sbits, int zero_key,
+                                         const uint64_t* __restrict__ list, uint32_t nl) {
+  if (k == 0) return zero_key != 0;
+  if (set) {
+    const uint32_t mask = (1u << sbits) - 1;
+    for (uint32_t h = (uint32_t)((k * kGolden) >> (64 - sbits));; h = (h + 1) & mask) {
+      const uint64_t v = set[h];
+      if (v == k) return true;
+      if (v == 0) break;
+    }
+  }
+  uint32_t lo = 0, len = nl;
+  while (len > 0) {
+    const uint32_t half = len >> 1;
+    if (list[lo + half] < k) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo < nl && list[lo] == k;
+}
+
+constexpr uint64_t kKey64FilterMax = 64;  // longer runs are left to the walk
+
+// thread per screen run: a short run keeps only [first, last] of the
+// positions whose 64-bit window key (257^W + the window's accumulator) is
+// in the sets; none: the run becomes empty
+__global__ void zc_key64_filter_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk, uint32_t W,
+                                       uint64_t pw, Run* __restrict__ runs, uint64_t nruns,
+                                       const uint64_t* __restrict__ set, uint32_t sbits, int zero_key,
+                                       const uint64_t* __restrict__ list, uint32_t nl) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nruns) return;
+  const Run r = runs[i];
+  if (r.end - r.start > kKey64FilterMax) return;
+  uint64_t first = ~0ull, last = 0;
+  for (uint64_t p = r.start; p < r.end; ++p) {
+    const uint64_t k = pw + rk_acc(data, blk, p + 1 - W, p + 1);
+    if (key64_in(k, set, sbits, zero_key, list, nl)) {
+      if (first == ~0ull) first = p;
+      last = p;
+    }
+  }
+  if (first == ~0ull) {
+    runs[i].end = r.start;
+  } else {
+    runs[i].start = first;
+    runs[i].end = last + 1;
   }
 }
 
@@ -2114,12 +2318,14 @@ hipError_t launch_range_digest(const uint8_t* data, uint64_t n, const uint64_t* 
 
 hipError_t launch_fscan(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                         uint64_t p_start, uint64_t p_end, uint64_t tile0, uint64_t ntiles, const uint32_t* f32,
-                        uint32_t nf, const uint32_t* fbits, Run* runs, uint64_t runs_cap, uint64_t* tile_off,
-                        uint32_t* tile_cnt, unsigned long long* counters, hipStream_t s) {
+                        uint32_t nf, const uint32_t* fbits, const uint32_t* bloom, uint32_t bloom_bits, Run* runs,
+                        uint64_t runs_cap, uint64_t* tile_off, uint32_t* tile_cnt, unsigned long long* counters,
+                        hipStream_t s) {
   if (!ntiles) return hipSuccess;
-  size_t dyn = nf > kFLinearMax ? kFBitmapWords * sizeof(uint32_t) : 0;
+  size_t dyn = !bloom && nf > kFLinearMax ? kFBitmapWords * sizeof(uint32_t) : 0;
   hipLaunchKernelGGL(zc_fscan_kernel, dim3((unsigned)ntiles), dim3(ZC_TPB), dyn, s, data, n, blk, W, pw32,
-                     p_start, p_end, tile0, f32, nf, fbits, runs, runs_cap, tile_off, tile_cnt, counters);
+                     p_start, p_end, tile0, f32, nf, fbits, bloom, bloom_bits, runs, runs_cap, tile_off, tile_cnt,
+                     counters);
   return hipGetLastError();
 }
 
@@ -2133,6 +2339,7 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
   hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(ZC_FTPB), 0, s, data, n, blk, W, pw32,     \
                      sbyte, p_start, p_end, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
   if (nfk == 1) ZC_FS(1);
+  else if (nfk == 64) ZC_FS(64);
   else if (nfk == 4) ZC_FS(4);
   else if (nfk == 16) ZC_FS(16);
   else if (nfk == 32) ZC_FS(32);
@@ -2166,6 +2373,46 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
     default: return launch_fscan_staged_q<3>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                              fbits17, runs, runs_cap, wt_off, wt_cnt, counters);
   }
+}
+
+hipError_t launch_fscan_staged_bloom(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
+                                     uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt,
+                                     const uint32_t* bloom, uint32_t bloom_bits, Run* runs, uint64_t runs_cap,
+                                     uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
+  if (!nwt) return hipSuccess;
+  if (W < 32 || n < 64 || p_end > n || (wt0 + nwt - 1) * ZC_FWT >= p_end || !bloom) return hipErrorInvalidValue;
+  FKeys K{};
+  K.bloom = bloom;
+  K.nk = bloom_bits;
+  K.pw64 = pow257_dev(W);
+  const uint32_t m = (16u - W % 16u) % 16u;
+  const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * (ZC_FTPB / 64));
+  const unsigned grid = (waves + ZC_FTPB / 64 - 1) / (ZC_FTPB / 64);
+  switch (m >> 2) {
+    case 0: return launch_fscan_staged_q<0>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+                                            nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
+    case 1: return launch_fscan_staged_q<1>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+                                            nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
+    case 2: return launch_fscan_staged_q<2>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+                                            nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
+    default: return launch_fscan_staged_q<3>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+                                             nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
+  }
+}
+
+hipError_t launch_bloom_add(uint32_t* bloom, uint32_t bits, const uint64_t* keys, uint32_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(zc_bloom_add_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, bloom, bits, keys, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_key64_filter(const uint8_t* data, const uint64_t* blk, uint32_t W, uint64_t pw, Run* runs,
+                               uint64_t nruns, const uint64_t* set, uint32_t sbits, int zero_key,
+                               const uint64_t* list, uint32_t nl, hipStream_t s) {
+  if (!nruns) return hipSuccess;
+  hipLaunchKernelGGL(zc_key64_filter_kernel, dim3(blocks_for(nruns, 64)), dim3(64), 0, s, data, blk, W, pw, runs,
+                     nruns, set, sbits, zero_key, list, nl);
+  return hipGetLastError();
 }
 
 hipError_t launch_sha1_grid(const uint8_t* data, uint64_t n, uint32_t W, uint32_t nr, uint8_t* out20,
