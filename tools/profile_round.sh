@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round profile set (run on the GPU box through gpurun; tooling only):
-#   bench lines (C2 with the CPU baseline, C3, C5, C2 end-to-end), rocprofv3
+#   bench lines (C2 with the CPU baseline and the value_sha1 / end_to_end / feed
+#   passes, C3, C5, C2 with SHA-1 ids as the headline), rocprofv3
 #   kernel-trace summaries of C2/C3/C5, the scan's FETCH_SIZE and WRITE_SIZE
 #   passes (separate runs), and the host CPU description.
 #   bash tools/profile_round.sh OUTDIR
@@ -9,17 +10,16 @@ OUT=${1:-gpurun_out/prof_round}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 240 python3 bench.py > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
-timeout -k 10 120 python3 bench.py --config c3 --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
-timeout -k 10 120 python3 bench.py --config c5 --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
-timeout -k 10 240 python3 bench.py --e2e --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
-timeout -k 10 240 python3 bench.py --sha1 --no-cpu-baseline >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
+timeout -k 10 120 python3 bench.py --config c3 --no-cpu-baseline --no-extras >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
+timeout -k 10 120 python3 bench.py --config c5 --no-cpu-baseline --no-extras >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
+timeout -k 10 240 python3 bench.py --sha1 --no-cpu-baseline --no-extras >> "$OUT/bench.jsonl" 2>> "$OUT/bench.err"
 for c in c2 c3 c5; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace_$c" -o $c -- \
-    python3 bench.py --config $c --steps 10 --no-cpu-baseline > "$OUT/trace_$c.log" 2>&1
+    python3 bench.py --config $c --steps 10 --no-cpu-baseline --no-extras > "$OUT/trace_$c.log" 2>&1
 done
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o f -- \
-  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
+  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > "$OUT/pmc_fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o w -- \
-  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
+  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > "$OUT/pmc_write.log" 2>&1
 (lscpu; echo; echo "nproc: $(nproc)") > "$OUT/host_cpu.txt"
 echo done

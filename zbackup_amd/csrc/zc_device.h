@@ -146,7 +146,7 @@ struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
 // CNT_FOVF: screen-run buffer overflow flag; CNT_ANCLESS: class leaders
 // without an anchor; CNT_CLASS: refs that are not the leader of their class
 enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_ANCLESS = 5, CNT_CLASS = 6,
-       CNT_LAST = 8 };
+       CNT_PAIRS = 7, CNT_LAST = 8 };
 
 // --- launchers (return hipError_t of the launch) ---------------------------
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
@@ -195,6 +195,7 @@ struct EpochIndex {
   uint32_t* gfilt;
   uint32_t* ancless;
   unsigned long long* counters;
+  uint2* pairs;  // scratch: nref {ref, leader} pairs for the byte check
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
@@ -225,12 +226,15 @@ hipError_t launch_slide_dir(uint32_t* base, const uint32_t* cnt_arr, uint32_t cn
 
 // every anchor of wave-tiles [wt0, wt0 + nwt) probes the filter, then the
 // table; candidate windows start at >= r (the reset point) and end before p_end
-// (the table holds every ref with an anchor; candidates name class leaders)
+// (the table holds every ref with an anchor; candidates name class leaders, and
+// leave out windows that are a grid chunk r_e + j W (j < nspec, ref nconf + j)
+// of the candidate's class: the walk takes those at the grid)
 // (tab may be null: the historic table alone; ht.tab null: none)
 hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
                         uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint32_t* cls,
                         const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W,
-                        const HistTab& ht, Cand* cand, uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
+                        const HistTab& ht, uint64_t r_e, uint32_t nconf, uint32_t nspec, Cand* cand,
+                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,

@@ -349,6 +349,7 @@ struct zc_ctx {
   DevBuf<uint32_t> fwt_cnt;
   DevBuf<Run> runs;
   DevBuf<uint32_t> ancless;
+  DevBuf<uint2> cpairs;  // content-class pairs to byte-check
   HostBuf<unsigned long long> h_cnt;
   HostBuf<unsigned long long> h_scnt;  // the scan's counters, read back with the first epoch's batch
   HostBuf<uint64_t> h_pre;             // digests of the predicted tail pieces
@@ -978,10 +979,11 @@ class Resolver {
         // content classes: identical refs share one leader in the table
         c_.ckeys.ensure(1u << tbits);
         c_.c_cls.ensure(nref_);
+        c_.cpairs.ensure(nref_);
         const EpochIndex ix{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
                             c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
                             c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
-                            c_.gfilt.p,   c_.ancless.p, c_.counters.p};
+                            c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p};
         HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
       } else {
         HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
@@ -993,7 +995,7 @@ class Resolver {
       const uint64_t* tab = nref_ && anchors ? c_.tab.p : nullptr;
       if (anchors)
         HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
-                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, c_.cand.p, c_.cand.cap, c_.counters.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
                          c_.stream));
       HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
       if (nsref)
@@ -1016,7 +1018,7 @@ class Resolver {
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
         HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
-                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, c_.cand.p, c_.cand.cap, c_.counters.p,
+                         c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
                          c_.stream));
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
@@ -1048,11 +1050,14 @@ class Resolver {
       }
     }
     if (!c_.smap.empty()) f_min_vis_ = 0;
-    if (!fmap_.empty() || !c_.smap.empty()) {
-      auto tf = Clock::now();
-      fscan();
-      c_.stats.fscan_ms += ms_since(tf);
-    }
+    has_f_ = !fmap_.empty() || !c_.smap.empty();
+    fs_ready_ = false;
+    fs_hi_ = x0();
+    // by-value keys (the static index) can match anywhere: the whole epoch at
+    // once; the epoch's own anchorless chunks mostly match at the grid (the
+    // walk's shortcut), so their screen grows from a short first block
+    fs_len_ = c_.smap.empty() ? std::max<uint64_t>(4ull << 20, 16ull * W_) : h_end_;
+    grid_shortcuts();
     auto tw = Clock::now();
     bool again = walk();
     c_.stats.walk_ms += ms_since(tw);
@@ -1247,26 +1252,29 @@ class Resolver {
   // are trimmed on the device to positions whose exact 64-bit key is in the
   // set before they come back (the filter's false hits never reach the walk)
   static constexpr size_t kLdsKeys = 2048;
-  void fscan() {
-    std::vector<uint32_t> keys32;
+  void fscan_setup() {
+    keys32_.clear();
+    std::vector<uint32_t>& keys32 = keys32_;
     for (auto& kv : fmap_) keys32.push_back((uint32_t)kv.first);
-    const bool bloom = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN) &&
+    bloom_ = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN) &&
                        c_.smap.size() + fmap_.size() > kLdsKeys;
+    const bool bloom = bloom_;
     if (!bloom)
       for (auto& kv : c_.smap) keys32.push_back((uint32_t)kv.first);
     std::sort(keys32.begin(), keys32.end());
     keys32.erase(std::unique(keys32.begin(), keys32.end()), keys32.end());
-    const uint32_t nf = bloom ? (uint32_t)(c_.smap.size() + keys32.size()) : (uint32_t)keys32.size();
+    nf_ = bloom ? (uint32_t)(c_.smap.size() + keys32.size()) : (uint32_t)keys32.size();
+    const uint32_t nf = nf_;
     c_.f32.ensure(std::max<size_t>(keys32.size(), 1));
     h2d(c_, c_.f32.p, keys32.data(), keys32.size());
     c_.fbits.ensure(1u << 14);
-    const uint32_t* bloom_p = nullptr;
+    bloom_p_ = nullptr;
     if (bloom) {
       statics_screen(c_);
       std::vector<uint32_t> bits = c_.sc_fbits;
       for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
       h2d(c_, c_.fbits.p, bits.data(), bits.size());
-      bloom_p = c_.bloom_s.p;
+      bloom_p_ = c_.bloom_s.p;
       std::vector<uint64_t> fk;
       for (auto& kv : fmap_) fk.push_back(kv.first);
       std::sort(fk.begin(), fk.end());
@@ -1278,14 +1286,21 @@ class Resolver {
         HCK(hipMemcpyAsync(c_.bloom_w.p, c_.bloom_s.p, (2 * sizeof(uint32_t)) << c_.bloom_bits,
                            hipMemcpyDeviceToDevice, c_.stream));
         HCK(launch_bloom_add(c_.bloom_w.p, c_.bloom_bits, c_.flist.p, (uint32_t)fk.size(), c_.stream));
-        bloom_p = c_.bloom_w.p;
+        bloom_p_ = c_.bloom_w.p;
       }
     } else if (nf > 16) {
       std::vector<uint32_t> bits(1u << 14, 0);
       for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
       h2d(c_, c_.fbits.p, bits.data(), bits.size());
     }
-    const uint64_t p_start = x0(), p_end = h_end_;
+  }
+
+  // screen positions [p_start, p_end) and append their runs to runs_
+  void fscan_range(uint64_t p_start, uint64_t p_end) {
+    const std::vector<uint32_t>& keys32 = keys32_;
+    const bool bloom = bloom_;
+    const uint32_t nf = nf_;
+    const uint32_t* bloom_p = bloom_p_;
     if (p_start >= p_end) return;
     const uint32_t pw32 = (uint32_t)pow257(W_);
     const uint64_t ntiles = (p_end + ZC_TILE - 1) / ZC_TILE;  // zc_fscan tiles up to the horizon
@@ -1293,7 +1308,10 @@ class Resolver {
     // from p_start to the end); zc_fscan redoes wave-tiles whose runs
     // overflowed, or everything when the staged kernel does not apply
     const uint64_t t_first = p_start / ZC_TILE;
-    const bool staged = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN);
+    // the staged kernel's wave walks a 512 KiB wave-tile (~0.5 ms); short
+    // ranges (the walk's first blocks) take the lane-per-KiB kernel
+    const bool staged = W_ >= 32 && n_ >= 64 && !(c_.flags & ZC_FLAG_NO_STAGED_SCREEN) &&
+                        p_end - p_start > (64ull << 20);
     const uint64_t wt_lo = staged ? p_start / ZC_FWT : 0;
     const uint64_t wt_hi = staged ? (p_end + ZC_FWT - 1) / ZC_FWT : 0;
     constexpr uint64_t kTpw = ZC_FWT / ZC_TILE;  // zc_fscan tiles per screen wave-tile
@@ -1405,8 +1423,16 @@ class Resolver {
       else
         take(&raw[woff[i]], wcnt[i]);
     }
-    has_f_ = !runs_.empty();
   }
+  std::vector<uint32_t> keys32_;
+  bool bloom_ = false;
+  uint32_t nf_ = 0;
+  const uint32_t* bloom_p_ = nullptr;
+  // the screen runs lazily: positions [x0, fs_hi_) are screened so far, in
+  // blocks of fs_len_ bytes (doubling) as the walk needs them
+  bool fs_ready_ = false;
+  uint64_t fs_hi_ = 0, fs_len_ = 0;
+  static constexpr uint64_t kFewPositions = 8;  // one fbatch (its first 8 positions per run)
 
   // first position p >= from inside the screen runs, or kInf
   size_t irun_ = 0;
@@ -1572,15 +1598,76 @@ class Resolver {
     return false;
   }
 
+  // the first screen position in [x, limit) that matches, or kInf; screens
+  // further as it goes (the runs below fs_hi_ are known)
   uint64_t next_f(uint64_t x, uint64_t limit, uint64_t* key) {
     if (!has_f_) return kInf;
     uint64_t p = std::max(x, f_min_vis_);
+    limit = std::min(limit, h_end_);
     for (;;) {
-      p = next_run_pos(p);
-      if (p == kInf || p >= limit) return kInf;
-      if (eval_f(p, key)) return p;
-      ++p;
+      if (p >= limit) return kInf;
+      const uint64_t q = next_run_pos(p);
+      if (q != kInf) {
+        if (q >= limit) return kInf;
+        if (eval_f(q, key)) return q;
+        p = q + 1;
+        continue;
+      }
+      if (fs_hi_ >= limit) return kInf;
+      const uint64_t lo = std::max(fs_hi_, p);
+      if (limit - lo <= kFewPositions) {
+        // a few positions (the walk's next candidate is close): each one is
+        // checked by eval_f's exact 64-bit key instead of a screen launch
+        runs_.push_back(Run{lo, limit});
+        fs_hi_ = limit;
+        continue;
+      }
+      auto tf = Clock::now();
+      if (!fs_ready_) {
+        fscan_setup();
+        fs_ready_ = true;
+      }
+      const uint64_t hi = std::min(h_end_, lo + fs_len_);
+      fscan_range(lo, hi);
+      fs_hi_ = hi;
+      fs_len_ *= 4;
+      c_.stats.fscan_ms += ms_since(tf);
     }
+  }
+
+  // Grid chunks of this epoch that are not the leader of their content class:
+  // the window that IS such a chunk matches at its end whenever a member of
+  // its class is in the index by then (cut earlier, or confirmed) and not
+  // consumed -- the earliest probe there, found without the probe's or the
+  // screen's candidates (the probe leaves those candidates out).  The walk
+  // takes them in order.
+  std::vector<uint32_t> sc_list_;
+  size_t isc_ = 0;
+  void grid_shortcuts() {
+    sc_list_.clear();
+    isc_ = 0;
+    if (cls_.empty()) return;
+    for (uint32_t j = 0; j < nspec_; ++j)
+      if (cls_[nconf_ + j] != nconf_ + j) sc_list_.push_back(j);
+  }
+  // the next grid window end >= x that matches (its grid chunk via *g), or kInf
+  uint64_t next_grid(uint64_t x, uint32_t* g) {
+    while (isc_ < sc_list_.size()) {
+      const uint32_t j = sc_list_[isc_];
+      const uint64_t pg = r_e_ + (uint64_t)(j + 1) * W_ - 1;
+      if (pg >= h_end_) return kInf;
+      if (pg >= x) {
+        const uint32_t gr = nconf_ + j;
+        // consumption only grows, so a class not in the index at pg now
+        // never will be
+        if (!dead_[gr] && class_alive_visible(cls_[gr], pg)) {
+          *g = gr;
+          return pg;
+        }
+      }
+      ++isc_;
+    }
+    return kInf;
   }
 
   // ---------------------------------------------------------------- walk
@@ -1676,6 +1763,47 @@ class Resolver {
     return true;
   }
 
+  // After a grid shortcut match of grid chunk j: the following grid chunks
+  // in a row that match at their own ends too (x is each one's end, so nothing
+  // can come first) -- a duplicated or constant stretch -- as one run of DUP
+  // records, written in parallel when long
+  void chain(uint64_t j) {
+    uint32_t jn = (uint32_t)j + 1;
+    while (isc_ + 1 < sc_list_.size() && sc_list_[isc_ + 1] == jn) {
+      const uint64_t pn = r_e_ + (uint64_t)(jn + 1) * W_ - 1;
+      if (pn >= h_end_) break;
+      const uint32_t gn = nconf_ + jn;
+      if (dead_[gn] || !class_alive_visible(cls_[gn], pn)) break;
+      ++isc_;
+      dead_[gn] = 1;
+      ++ndead_;
+      ++jn;
+    }
+    const uint64_t nchain = jn - (j + 1);
+    if (!nchain) return;
+    const size_t o = c_.recs.size();
+    c_.recs.resize(o + nchain);
+    zc_record* out = c_.recs.data() + o;
+    const uint64_t k0 = j + 1, r0 = r_e_;
+    const uint32_t W = W_;
+    const uint64_t* key = c_.h_key.p;
+    auto fill = [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; ++i) {
+        zc_record& r = out[i];
+        r.offset = r0 + (k0 + i) * W;
+        r.size = W;
+        r.kind = ZC_CHUNK_DUP;
+        r.rolling = key[k0 + i];
+        memset(r.sha1, 0, sizeof r.sha1);
+      }
+    };
+    if (nchain >= kParallelRecords) HostPool::get().run(nchain, fill);
+    else fill(0, nchain);
+    r_ = r_e_ + (uint64_t)jn * W_;
+    s_ = r_;
+    if (jn > ks_) ks_ = jn;
+  }
+
   // the probes of this epoch are done up to h_end_: go on at a horizon, stop
   // at the end of a window segment (the state carries over to the next one),
   // or finish the stream
@@ -1697,6 +1825,8 @@ class Resolver {
     irun_ = 0;
     for (;;) {
       if (x >= h_end_) return stop();
+      uint32_t gref = 0;
+      const uint64_t pg = next_grid(x, &gref);
       uint64_t pa = kInf;
       uint32_t refa = 0;
       while (ia < acands_.size()) {
@@ -1711,14 +1841,18 @@ class Resolver {
       // historic entries are always in the index
       while (ih < hcands_.size() && hcands_[ih].p < x) ++ih;
       const uint64_t ph = ih < hcands_.size() ? hcands_[ih].p : kInf;
-      const uint64_t pe = std::min(pa, ph);
+      const uint64_t pe = std::min(std::min(pa, ph), pg);
       uint64_t fkey = 0;
-      uint64_t pf = next_f(x, pe == kInf ? h_end_ : pe + 1, &fkey);
+      // nothing precedes a match at x itself
+      uint64_t pf = pe == x ? kInf : next_f(x, pe == kInf ? h_end_ : pe + 1, &fkey);
       if (pe == kInf && pf == kInf) return stop();
       uint64_t m, key;
       if (pf != kInf && (pe == kInf || pf < pe)) {
         m = pf;
         key = fkey;
+      } else if (pg <= pa && pg <= ph) {
+        m = pg;
+        key = ref_key(gref);
       } else if (pa <= ph) {
         m = pa;
         key = ref_key(refa);
@@ -1741,6 +1875,7 @@ class Resolver {
           ++ndead_;
         }
         if (j >= ks_) ks_ = j + 1;
+        if (m == pg) chain(j);
         x = r_ + W_ - 1;
         continue;
       }

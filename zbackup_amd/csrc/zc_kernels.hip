@@ -932,11 +932,17 @@ constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
 // another.
 constexpr int kProbeTPB = 256;
 
+// the epoch's grid: chunk j starts at r_e + j W (ref nconf + j), j < nspec
+struct EpochGrid {
+  uint64_t r_e;
+  uint32_t nconf, nspec;
+};
+
 __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
                                              const uint64_t* __restrict__ tab, uint32_t tbits,
                                              const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
                                              const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead,
-                                             uint64_t r, uint64_t n, uint32_t W,
+                                             uint64_t r, uint64_t n, uint32_t W, const EpochGrid& eg,
                                              Cand* __restrict__ cand, uint64_t cand_cap,
                                              unsigned long long* __restrict__ counters) {
   if (pos < r + ZC_ANCHOR_MIN_OFF || !tab) return;
@@ -954,7 +960,14 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
         const uint64_t o = anc_off[ref];
         if (pos >= r + o) {
           const uint64_t ws = pos - o, p = ws + W - 1;
-          if (p < n && p >= vis[ref] && !dead[ref]) {
+          // a window that is a grid chunk of this epoch in ref's class is the
+          // walk's (grid shortcut): no candidate
+          bool grid_twin = false;
+          if (ws >= eg.r_e && (ws - eg.r_e) % W == 0) {
+            const uint64_t j = (ws - eg.r_e) / W;
+            grid_twin = j < eg.nspec && cls[eg.nconf + j] == ref;
+          }
+          if (p < n && p >= vis[ref] && !dead[ref] && !grid_twin) {
             const unsigned long long c = atomicAdd(&counters[CNT_CAND], 1ull);
             if (c < cand_cap) {
               cand[c].p = p;
@@ -1009,7 +1022,7 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const uint8_t* __restrict__ data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* __restrict__ tab,
     uint32_t tbits, const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off,
     const uint32_t* __restrict__ cls, const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r,
-    uint64_t n, uint32_t W, HistTab ht,
+    uint64_t n, uint32_t W, HistTab ht, EpochGrid eg,
     Cand* __restrict__ cand, uint64_t cand_cap, unsigned long long* __restrict__ counters) {
   const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
@@ -1066,7 +1079,7 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const uint32_t t = (a.x >> 24) & 63u;
     const uint64_t pos = ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu);
     if (a.x & (1u << 30))
-      probe_anchor(data, pos, a.y, tab, tbits, anc_off, cls, vis, dead, r, n, W, cand, cand_cap, counters);
+      probe_anchor(data, pos, a.y, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, cand, cand_cap, counters);
     if (a.x & (1u << 31)) probe_hist(data, pos, a.y, ht, r, n, W, cand, cand_cap, counters);
   }
   // wave-tiles with more anchors than the slots above
@@ -1077,7 +1090,7 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
       const uint32_t fb = gk & ((1u << kGFiltBits) - 1);
       const uint64_t pos = (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e];
       if (gfilt && ((gfilt[fb >> 5] >> (fb & 31)) & 1u))
-        probe_anchor(data, pos, gk, tab, tbits, anc_off, cls, vis, dead, r, n, W, cand, cand_cap, counters);
+        probe_anchor(data, pos, gk, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, cand, cand_cap, counters);
       if (ht.tab && ((ht.filt[fb >> 5] >> (fb & 31)) & 1u))
         probe_hist(data, pos, gk, ht, r, n, W, cand, cand_cap, counters);
     }
@@ -1113,6 +1126,33 @@ __device__ __forceinline__ bool wave_ranges_equal(const uint8_t* __restrict__ da
   // ragged tail (len not a multiple of 16)
   const uint32_t tail0 = len & ~15u;
   for (uint32_t j = tail0 + lane; j < len; j += 64) diff |= data[a + j] != data[b + j];
+  return !__any(diff);
+}
+
+// The same with the 8 KiB steps taken in a rotated order (len a multiple of
+// 8 KiB): many waves comparing against ONE range (a content class's leader,
+// the zero chunk of an all-zero stream) then read different lines of it at
+// any moment instead of hammering the same L2 channel.
+__device__ __forceinline__ bool wave_ranges_equal_rot(const uint8_t* __restrict__ data, uint64_t a, uint64_t b,
+                                                      uint32_t len, uint32_t lane, uint32_t rot) {
+  constexpr uint32_t kStep = 8 * 64 * 16;
+  if (len % kStep) return wave_ranges_equal(data, a, b, len, lane);
+  const uint32_t nst = len / kStep;
+  bool diff = false;
+  for (uint32_t t = 0; t < nst; ++t) {
+    uint32_t tt = t + rot % nst;
+    tt = tt >= nst ? tt - nst : tt;
+    const uint32_t i = tt * kStep + lane * 16;
+    uint4 x[8], y[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      __builtin_memcpy(&x[k], data + a + i + k * 1024, 16);
+      __builtin_memcpy(&y[k], data + b + i + k * 1024, 16);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      diff |= (x[k].x != y[k].x) | (x[k].y != y[k].y) | (x[k].z != y[k].z) | (x[k].w != y[k].w);
+  }
   return !__any(diff);
 }
 
@@ -1212,42 +1252,53 @@ __global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint
   }
 }
 
-// thread per ref: its class = the lowest ref with the same key if the bytes
-// are equal, else itself (the wave compares the bytes of each of its refs
-// that is not that lowest ref, one range pair at a time); class leaders
-// without an anchor are listed for the exact screen
-__global__ void __launch_bounds__(256) zc_class_resolve_kernel(
-    const uint8_t* __restrict__ data, const uint64_t* __restrict__ key, const uint64_t* __restrict__ start,
-    const uint32_t* __restrict__ anc_off, uint32_t nref, uint32_t W, const uint64_t* __restrict__ ckeys,
-    uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
-    unsigned long long* __restrict__ counters) {
+// Content classes in two launches.  zc_class_lead_kernel, thread per ref: the
+// lowest ref with its key (its leader candidate); cls = itself for now; a
+// leader without an anchor is listed for the exact screen; a ref with a lower
+// equal-key ref is listed as a pair {ref, leader} for the byte check.
+// zc_class_verify_kernel, persistent waves over the pairs, one pair per wave
+// at a time (eight 16-byte loads per side in flight per lane): equal bytes ->
+// cls = leader (counters[CNT_CLASS]++); else a ref without an anchor is listed
+// for the screen.  Every pair's bytes are read once, all pairs side by side.
+__global__ void __launch_bounds__(256) zc_class_lead_kernel(
+    const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off, uint32_t nref,
+    const uint64_t* __restrict__ ckeys, uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
+    uint2* __restrict__ pairs, unsigned long long* __restrict__ counters) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63;
-  const bool valid = i < nref;
-  uint32_t lead = i;
-  if (valid) {
-    const uint64_t k = key[i];
-    const uint32_t mask = (1u << cbits) - 1;
-    uint32_t h = key_slot(k, cbits);
-    uint64_t w;
-    for (;; h = (h + 1) & mask) {  // the key's slot: equal high word and an equal key at its ref
-      w = ckeys[h];
-      if ((w >> 32) == (k >> 32) && key[(uint32_t)w] == k) break;
-    }
-    lead = (uint32_t)w;
-    cls[i] = i;
-    if (lead == i && anc_off[i] == ZC_NO_ANCHOR) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = i;
+  if (i >= nref) return;
+  const uint64_t k = key[i];
+  const uint32_t mask = (1u << cbits) - 1;
+  uint32_t h = key_slot(k, cbits);
+  uint64_t w;
+  for (;; h = (h + 1) & mask) {  // the key's slot: equal high word and an equal key at its ref
+    w = ckeys[h];
+    if ((w >> 32) == (k >> 32) && key[(uint32_t)w] == k) break;
   }
-  for (uint64_t m = __ballot(valid && lead != i); m; m &= m - 1) {
-    const int l = __builtin_ctzll(m);
-    const uint32_t ri = __shfl(i, l), rl = __shfl(lead, l);
-    const bool same = wave_ranges_equal(data, start[ri], start[rl], W, lane);
+  const uint32_t lead = (uint32_t)w;
+  cls[i] = i;
+  if (lead == i) {
+    if (anc_off[i] == ZC_NO_ANCHOR) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = i;
+  } else {
+    pairs[atomicAdd(&counters[CNT_PAIRS], 1ull)] = make_uint2(i, lead);
+  }
+}
+
+__global__ void __launch_bounds__(256) zc_class_verify_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ start, const uint32_t* __restrict__ anc_off,
+    uint32_t W, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless, const uint2* __restrict__ pairs,
+    unsigned long long* __restrict__ counters) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t np = counters[CNT_PAIRS];
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; q < np; q += nw) {
+    const uint2 pr = pairs[q];
+    const bool same = wave_ranges_equal_rot(data, start[pr.x], start[pr.y], W, lane, (uint32_t)q);
     if (lane == 0) {
       if (same) {
-        cls[ri] = rl;
+        cls[pr.x] = pr.y;
         atomicAdd(&counters[CNT_CLASS], 1ull);
-      } else if (anc_off[ri] == ZC_NO_ANCHOR) {
-        ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = ri;
+      } else if (anc_off[pr.x] == ZC_NO_ANCHOR) {
+        ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = pr.x;
       }
     }
   }
@@ -2237,8 +2288,12 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
   if (!nref) return hipGetLastError();
   hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
                      ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
-  hipLaunchKernelGGL(zc_class_resolve_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, data, ix.key, ix.start,
-                     ix.anc, nref, W, ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.counters);
+  hipLaunchKernelGGL(zc_class_lead_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, nref,
+                     ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.pairs, ix.counters);
+  // persistent: up to 16 waves per CU (the pair count is on the device)
+  const unsigned vblocks = (unsigned)std::min<uint64_t>(blocks_for(nref, 4), (uint64_t)cu_count() * 4);
+  hipLaunchKernelGGL(zc_class_verify_kernel, dim3(vblocks), dim3(256), 0, s, data, ix.start, ix.anc, W, ix.cls,
+                     ix.ancless, ix.pairs, ix.counters);
   return hipGetLastError();
 }
 
@@ -2271,8 +2326,10 @@ hipError_t launch_slide_dir(uint32_t* base, const uint32_t* cnt_arr, uint32_t cn
 hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* tab,
                         uint32_t tbits, const uint32_t* gfilt, const uint32_t* anc_off, const uint32_t* cls,
                         const uint64_t* vis, const uint8_t* dead, uint64_t r, uint64_t p_end, uint32_t W,
-                        const HistTab& ht, Cand* cand, uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
+                        const HistTab& ht, uint64_t r_e, uint32_t nconf, uint32_t nspec, Cand* cand,
+                        uint64_t cand_cap, unsigned long long* counters, hipStream_t s) {
   if (!nwt || (!tab && !ht.tab)) return hipSuccess;
+  const EpochGrid eg{r_e, nconf, nspec};
   if (!tab) gfilt = nullptr;
   // 4 wave-tiles per wave, 2 slots per lane each (128 anchors per wave-tile
   // before the extra loop; 64 expected at W = 64 KiB): 60 us per 8 GiB vs 68
@@ -2281,8 +2338,8 @@ hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64
   constexpr int kWT = 4, kSlots = 2;
   const uint64_t waves = (nwt + kWT - 1) / kWT;
   hipLaunchKernelGGL((zc_probe_kernel<kWT, kSlots>), dim3(blocks_for(waves * 64, kProbeTPB)), dim3(kProbeTPB), 0, s,
-                     data, av, wt0, nwt, tab, tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, ht, cand, cand_cap,
-                     counters);
+                     data, av, wt0, nwt, tab, tbits, gfilt, anc_off, cls, vis, dead, r, p_end, W, ht, eg, cand,
+                     cand_cap, counters);
   return hipGetLastError();
 }
 
