@@ -1137,17 +1137,19 @@ __device__ __forceinline__ bool wave_ranges_equal_rot(const uint8_t* __restrict_
                                                       uint32_t len, uint32_t lane, uint32_t rot) {
   constexpr uint32_t kStep = 8 * 64 * 16;
   if (len % kStep) return wave_ranges_equal(data, a, b, len, lane);
-  const uint32_t nst = len / kStep;
+  // 1 KiB blocks, eight per step, the block order rotated by `rot`
+  const uint32_t nb = len / 1024;
+  uint32_t blk0 = rot % nb;
   bool diff = false;
-  for (uint32_t t = 0; t < nst; ++t) {
-    uint32_t tt = t + rot % nst;
-    tt = tt >= nst ? tt - nst : tt;
-    const uint32_t i = tt * kStep + lane * 16;
+  for (uint32_t t = 0; t < nb; t += 8) {
     uint4 x[8], y[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      __builtin_memcpy(&x[k], data + a + i + k * 1024, 16);
-      __builtin_memcpy(&y[k], data + b + i + k * 1024, 16);
+      uint32_t bk = blk0 + t + k;
+      bk = bk >= nb ? bk - nb : bk;
+      const uint32_t i = bk * 1024 + lane * 16;
+      __builtin_memcpy(&x[k], data + a + i, 16);
+      __builtin_memcpy(&y[k], data + b + i, 16);
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -1290,18 +1292,20 @@ __global__ void __launch_bounds__(256) zc_class_verify_kernel(
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t np = counters[CNT_PAIRS];
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  unsigned long long joined = 0;  // one counter atomic per wave, not per pair
   for (uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; q < np; q += nw) {
     const uint2 pr = pairs[q];
     const bool same = wave_ranges_equal_rot(data, start[pr.x], start[pr.y], W, lane, (uint32_t)q);
     if (lane == 0) {
       if (same) {
         cls[pr.x] = pr.y;
-        atomicAdd(&counters[CNT_CLASS], 1ull);
+        ++joined;
       } else if (anc_off[pr.x] == ZC_NO_ANCHOR) {
         ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = pr.x;
       }
     }
   }
+  if (lane == 0 && joined) atomicAdd(&counters[CNT_CLASS], joined);
 }
 
 // ---------------------------------------------------------------------------
