@@ -40,6 +40,8 @@ CONFIGS = {
     "c2": "C2: 1 x 8 GiB seeded random stream, device-resident, W=65536",
     "c3": "C3: 8 GiB = two copies of a 4 GiB seeded random block, W=65536",
     "c5": "C5: 8 GiB all-zero stream, W=65536",
+    "edit": "edited duplicate: 4 GiB seeded random, then the same 4 GiB with 1-100 random bytes inserted "
+            "every 1 MiB (~4096 grid shifts), 8 GiB in all, W=65536",
 }
 C4 = "C4: N x 8 GiB independent seeded random streams, one per GPU, W=65536"
 
@@ -168,9 +170,37 @@ def pmc_traffic(n_bytes):
         return None
 
 
+def fill_edited(torch, buf, n, seed, local):
+    """4 GiB seeded random block A, then A again in 1 MiB pieces each followed
+    by 1-100 random bytes, cut at n bytes (the grid moves at every insertion)."""
+    from zbackup_amd import fill_splitmix64
+    import numpy as np
+    half = n // 2
+    fill_splitmix64(buf.data_ptr(), half, seed, local)
+    rng = np.random.default_rng(seed)
+    noise = torch.empty(1 << 20, dtype=torch.uint8, device=buf.device)
+    fill_splitmix64(noise.data_ptr(), noise.numel(), seed + 7919, local)
+    pos, src, piece = half, 0, 1 << 20
+    while pos < n:
+        ln = min(piece, half - src, n - pos)
+        if ln <= 0:
+            break
+        buf[pos:pos + ln].copy_(buf[src:src + ln])
+        pos += ln
+        src += ln
+        k = min(int(rng.integers(1, 101)), n - pos)
+        o = int(rng.integers(0, noise.numel() - 128))
+        buf[pos:pos + k].copy_(noise[o:o + k])
+        pos += k
+    if pos < n:
+        fill_splitmix64(buf.data_ptr() + pos, n - pos, seed + 1, local)
+
+
 def fill_stream(torch, buf, n, config, seed, local):
     from zbackup_amd import fill_splitmix64
-    if config == "c5":
+    if config == "edit":
+        fill_edited(torch, buf, n, seed, local)
+    elif config == "c5":
         buf.zero_()
     elif config == "c3":
         fill_splitmix64(buf.data_ptr(), n // 2, seed, local)

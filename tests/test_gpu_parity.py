@@ -336,3 +336,30 @@ def test_c5_all_zero_8gib(torch_cuda, big_random):
     assert recs["kind"][0] == 0 and (recs["kind"][1:] == 1).all()
     assert (recs["rolling"] == 0x172AEAFF81000001).all()
     assert np.array_equal(recs["offset"], np.arange(n // W64, dtype=np.uint64) * W64)
+
+
+# --- edited duplicates: a copy with small insertions every piece ------------
+# (each insertion moves the grid: backup_creator.cc:242-265 resets the window
+# on the match after it; the walk follows the new grid lazily)
+
+def edited_copy_spec(seed, block, piece, rng):
+    """R<seed>:<block> followed by the same bytes in `piece`-byte pieces, each
+    followed by 1-100 inserted random bytes."""
+    segs, off = [f"R{seed}:{block}"], 0
+    while off < block:
+        ln = min(piece, block - off)
+        segs.append(f"C{off}:{ln}")
+        segs.append(f"R{int(rng.integers(1, 1 << 30))}:{int(rng.integers(1, 101))}")
+        off += ln
+    return ",".join(segs)
+
+
+@pytest.mark.parametrize("W,block,piece", [(65536, 64 << 20, 1 << 20), (4096, 8 << 20, 64 << 10),
+                                           (1000, 2 << 20, 50000)])
+def test_edited_duplicate_vs_oracle(torch_cuda, W, block, piece):
+    rng = np.random.default_rng(W)
+    data = oracle.gen(edited_copy_spec(31, block, piece, rng))
+    want = oracle.chunk(data, W)
+    assert sum(1 for r in want if r[0] == "D") > block // W // 2
+    assert _run_device(torch_cuda, data, W) == want
+    assert _run_host_feed(data, W) == want

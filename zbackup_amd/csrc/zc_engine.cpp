@@ -940,6 +940,7 @@ class Resolver {
     fmap_.clear();
     fmemo_valid_ = false;
     fb_ = FBatch{};
+    fb_next_ = kInf;
     has_f_ = false;
     f_min_vis_ = kInf;
     uint64_t ncand = 0, nancless = 0;
@@ -1471,6 +1472,7 @@ class Resolver {
     return -1;
   }
 
+  uint64_t fb_take_ = 8, fb_next_ = kInf;
   void build_fbatch(uint64_t p0) {
     const auto t0 = Clock::now();
     FBatch b;
@@ -1484,8 +1486,15 @@ class Resolver {
     {
       size_t ir = irun_;
       while (ir < runs_.size() && runs_[ir].end <= p0) ++ir;
+      // a run whose positions keep failing (content with no live match, e.g.
+      // a long repeated run whose refs were consumed) takes 8x more of its
+      // positions per batch each time the walk comes back right after them
+      fb_take_ = p0 == fb_next_ ? std::min<uint64_t>(fb_take_ * 8, 1u << 16) : 8;
+      fb_next_ = kInf;
       for (; ir < runs_.size() && pos.size() < kFBatchMax / 2; ++ir) {
-        const uint64_t a = std::max(p0, runs_[ir].start), b = std::min(runs_[ir].end, a + 8);
+        const uint64_t a = std::max(p0, runs_[ir].start);
+        const uint64_t b = std::min(runs_[ir].end, a + (fb_next_ == kInf ? fb_take_ : 8));
+        if (fb_next_ == kInf) fb_next_ = b;
         for (uint64_t x = a; x < b; ++x) pos.push_back(x);
       }
     }
@@ -1658,9 +1667,10 @@ class Resolver {
       if (pg >= h_end_) return kInf;
       if (pg >= x) {
         const uint32_t gr = nconf_ + j;
-        // consumption only grows, so a class not in the index at pg now
-        // never will be
-        if (!dead_[gr] && class_alive_visible(cls_[gr], pg)) {
+        // (gr itself may be consumed -- then x is past pg -- or abandoned by a
+        // grid shift: its window still equals its class.)  Consumption only
+        // grows, so a class not in the index at pg now never will be
+        if (class_alive_visible(cls_[gr], pg)) {
           *g = gr;
           return pg;
         }
@@ -1773,7 +1783,7 @@ class Resolver {
       const uint64_t pn = r_e_ + (uint64_t)(jn + 1) * W_ - 1;
       if (pn >= h_end_) break;
       const uint32_t gn = nconf_ + jn;
-      if (dead_[gn] || !class_alive_visible(cls_[gn], pn)) break;
+      if (!class_alive_visible(cls_[gn], pn)) break;
       ++isc_;
       dead_[gn] = 1;
       ++ndead_;
@@ -1819,12 +1829,41 @@ class Resolver {
     return false;
   }
 
+  // Grid shifts without a new epoch.  A match that moves the grid (the window
+  // starts off the epoch's grid) ends the epoch's grid: its chunks not cut by
+  // then leave the index (abandoned: marked dead), and a new grid starts at
+  // r_g_.  The walk goes on with this epoch's candidates -- they cover every
+  // index entry but the new grid's chunks -- for as long as no chunk of the
+  // new grid gets cut: matches on it (an edited copy re-synchronising after
+  // each insertion) consume its chunks, and pieces under W never match.  The
+  // first time one would be cut (a match at or past s_ + 2W - 1, or the end
+  // of the epoch's probes), a real epoch starts from the current position:
+  // its index then holds the new grid's chunks.
+  bool lazy_ = false;
+  uint64_t r_g_ = 0;
+  void abandon(uint64_t m) {
+    for (uint32_t k = 0; k < nspec_; ++k) {
+      const uint32_t g = nconf_ + k;
+      if (ref_vis(g) > m && !dead_[g]) {
+        dead_[g] = 1;
+        ++ndead_;
+      }
+    }
+  }
+  bool lazy_exit(uint64_t x) {
+    keep_saved(x);
+    x_resume_ = x;
+    hspan_ = std::max<uint64_t>(kHorizon0, 64ull * W_);
+    return true;
+  }
+
   bool walk() {
     uint64_t x = x0();
     size_t ia = 0, ih = 0;
     irun_ = 0;
+    lazy_ = false;
     for (;;) {
-      if (x >= h_end_) return stop();
+      if (x >= h_end_) return lazy_ ? lazy_exit(x) : stop();
       uint32_t gref = 0;
       const uint64_t pg = next_grid(x, &gref);
       uint64_t pa = kInf;
@@ -1844,8 +1883,12 @@ class Resolver {
       const uint64_t pe = std::min(std::min(pa, ph), pg);
       uint64_t fkey = 0;
       // nothing precedes a match at x itself
-      uint64_t pf = pe == x ? kInf : next_f(x, pe == kInf ? h_end_ : pe + 1, &fkey);
-      if (pe == kInf && pf == kInf) return stop();
+      // lazily on a shifted grid, no match at or past s_ + 2W - 1 is taken
+      // (lazy_exit first): the screen search stops there
+      uint64_t flim = pe == kInf ? h_end_ : pe + 1;
+      if (lazy_) flim = std::min<uint64_t>(flim, s_ + 2ull * W_ - 1);
+      uint64_t pf = pe == x ? kInf : next_f(x, flim, &fkey);
+      if (pe == kInf && pf == kInf) return lazy_ ? lazy_exit(x) : stop();
       uint64_t m, key;
       if (pf != kInf && (pe == kInf || pf < pe)) {
         m = pf;
@@ -1860,6 +1903,8 @@ class Resolver {
         m = ph;
         key = c_.hkey[hcands_[ih].ref];
       }
+      // the new grid's next chunk [s_, s_ + W) would be cut first
+      if (lazy_ && m >= s_ + 2ull * W_ - 1) return lazy_exit(x);
       // the match at m
       save_grid_until(m);
       const uint64_t ws = m - W_ + 1;
@@ -1867,6 +1912,16 @@ class Resolver {
       push(ws, W_, ZC_CHUNK_DUP, key);
       r_ = m + 1;
       s_ = r_;
+      if (lazy_) {
+        // on the new grid: its chunk under the window is consumed; off it: the
+        // grid moves again (back onto this epoch's grid: a real epoch)
+        if ((r_ - r_g_) % W_ != 0) {
+          r_g_ = r_;
+          if ((r_g_ - r_e_) % W_ == 0) return lazy_exit(r_ + W_ - 1);
+        }
+        x = r_ + W_ - 1;
+        continue;
+      }
       if ((r_ - r_e_) % W_ == 0) {
         // same grid: the grid chunk the window covered is consumed, not saved
         const uint64_t j = (ws - r_e_) / W_;
@@ -1879,12 +1934,11 @@ class Resolver {
         x = r_ + W_ - 1;
         continue;
       }
-      // grid shift: keep the saved chunks of this epoch, start a new one
-      // (its horizon kHorizon0 ahead)
-      keep_saved(m);
-      x_resume_ = 0;
-      hspan_ = std::max<uint64_t>(kHorizon0, 64ull * W_);
-      return true;
+      // grid shift: this epoch's grid ends at m; the walk goes on lazily
+      abandon(m);
+      lazy_ = true;
+      r_g_ = r_;
+      x = r_ + W_ - 1;
     }
   }
 
