@@ -20,27 +20,17 @@ int main(int argc, char** argv) {
   uint64_t* blk; uint32_t *dbase, *dcnt, *prel, *pg; unsigned long long* cnt;
   CK(hipMalloc(&blk, n / ZC_SPAN * 8)); CK(hipMalloc(&dbase, nwt * 4)); CK(hipMalloc(&dcnt, nwt * 4));
   CK(hipMalloc(&prel, nwt * wcap * 4)); CK(hipMalloc(&pg, nwt * wcap * 4)); CK(hipMalloc(&cnt, 64));
-  const PoolOut po{dbase, dcnt, prel, pg, wcap};
+  const PoolOut po{dbase, dcnt, prel, pg, wcap, 0};
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
+  constexpr int P = kScanProduct;
   std::vector<V> vs = {
-    {"full", zc_scan_kernel<0>, {}},
-    {"full_no_atomic", zc_scan_kernel<ABL_NO_ATOMIC>, {}},
-    {"stage_only_no_atomic", zc_scan_kernel<ABL_NO_BYTES | ABL_NO_ATOMIC>, {}},
-    {"no_digest_no_atomic", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_ATOMIC>, {}},
-    {"no_record", zc_scan_kernel<ABL_NO_RECORD>, {}},
-    {"no_digest", zc_scan_kernel<ABL_NO_DIGEST>, {}},
-    {"no_digest_no_record", zc_scan_kernel<ABL_NO_DIGEST | ABL_NO_RECORD>, {}},
-    {"digest_only", zc_scan_kernel<ABL_NO_GEAR>, {}},
-    {"stage_only", zc_scan_kernel<ABL_NO_BYTES>, {}},
-    {"stage_only_no_tile_end", zc_scan_kernel<ABL_NO_BYTES | ABL_NO_TILE_END>, {}},
-    {"full_no_tile_end", zc_scan_kernel<ABL_NO_TILE_END>, {}},
-    {"gear_digest_nobranch", zc_scan_kernel<ABL_NO_BRANCH>, {}},
-    {"gear_nobranch", zc_scan_kernel<ABL_NO_BRANCH | ABL_NO_DIGEST>, {}},
-    {"full_never_taken", zc_scan_kernel<ABL_NEVER>, {}},
-    {"gear_never_taken", zc_scan_kernel<ABL_NEVER | ABL_NO_DIGEST>, {}},
-    {"te_digest_only", zc_scan_kernel<ABL_TE_DIGEST_ONLY>, {}},
-    {"stage_only_te_digest", zc_scan_kernel<ABL_NO_BYTES | ABL_TE_DIGEST_ONLY>, {}},
+    {"product (nt DMA)", zc_scan_kernel<P>, {}},
+    {"te_no_anchor_store", zc_scan_kernel<P | ABL_TE_NO_ANCHOR_STORE>, {}},
+    {"te_digest_only", zc_scan_kernel<P | ABL_TE_DIGEST_ONLY>, {}},
+    {"full_te_no_store", zc_scan_kernel<P | ABL_TE_NO_STORE>, {}},
+    {"stage_only", zc_scan_kernel<P | ABL_NO_BYTES>, {}},
+    {"stage_only_te_no_store", zc_scan_kernel<P | ABL_NO_BYTES | ABL_TE_NO_STORE>, {}},
   };
   for (int round = 0; round < 12; ++round)
     for (auto& v : vs) {

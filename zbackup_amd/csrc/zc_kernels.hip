@@ -203,7 +203,12 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 // 64 = no tile-end work (span digests, anchors to the pool), 128 = no
 // counter atomic, 256 = the tile end stores the span digests only
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128, ABL_TE_DIGEST_ONLY = 256 };
+       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128, ABL_TE_DIGEST_ONLY = 256,
+       ABL_DMA_NT = 512, ABL_DMA_SC1 = 1024, ABL_STAGGER_HALF = 2048, ABL_STAGGER_QUARTER = 4096,
+       ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768 };
+// the product's scan: the staging DMA is non-temporal (the stream is read
+// once; tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB)
+constexpr int kScanProduct = ABL_DMA_NT;
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
   uint32_t* e;      // {(rel of the piece >> 4) << 8 | the lane's previous entry, gear before the piece}
@@ -421,6 +426,7 @@ __host__ __device__ constexpr uint32_t row_swizzle(uint32_t row) { return (row /
 // built with scalar instructions): the lane's part of every instruction is
 // its loop-invariant 32-bit offset lane_off[j], so a round costs no vector
 // address arithmetic.  (wave must be wave-uniform: readfirstlane'd.)
+template <int AUX>
 __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, uint8_t* ring, uint32_t wave,
                                             const uint32_t (&lane_off)[kDmaRound], uint64_t tile, int r,
                                             uint32_t slot) {
@@ -431,7 +437,7 @@ __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, ui
 #pragma unroll
   for (int j = 0; j < kDmaRound; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + j * 1024), 16, (int)(lane_off[j] ^ flip), 0, 0,
-                                             0);
+                                             AUX);
 }
 
 template <int N>
@@ -548,6 +554,13 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
                                                   uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
                                                   unsigned long long* __restrict__ counters) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
+  if (ABL & ABL_TE_NO_STORE) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int t = 0; t < kDigests; ++t) x ^= (uint32_t)bk[t] ^ (uint32_t)(bk[t] >> 32);
+    asm volatile("" ::"v"(x));
+    return 0;
+  }
 #pragma unroll
   for (int t = 0; t < kDigests / 2; ++t)
     bo[t] = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
@@ -555,7 +568,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   if (ABL & ABL_TE_DIGEST_ONLY) return kDigests / 2;
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)(wt - po.wt0) * po.wcap;
-  uint32_t tot = 0, excl = 0;
+  uint32_t tot = 0, excl = 0, nst = 0;
   bool over = wl.n > ZC_WLIST;
   if (!over) {
     uint32_t cnt = 0, cnt_lo = 0;  // cnt_lo: anchors in the span's first half
@@ -573,20 +586,39 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
       // one taken first)
       const uint32_t sbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
       uint32_t k_lo = excl + cnt_lo, k_hi = excl + cnt;
-      for (uint32_t i = last; i != kNoEntry;) {
-        const uint32_t e0 = wl.e[2 * i];
-        const uint32_t rel = ((e0 >> 8) & 0xFFu) << 4;
-        uint32_t mask = e0 >> 16;
-        const uint4 v = wl.x[i];
-        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-        // the gear before each dword of the piece
-        uint32_t gd[4];
-        gd[0] = wl.e[2 * i + 1];
+      // one wave-uniform loop, one anchor per lane per pass, so the store
+      // instructions issued are counted exactly (nst): the next tile's first
+      // wait then leaves exactly them in flight instead of draining the
+      // round prefetched behind them
+      uint32_t i = last, mask = 0, w = 0, rel = 0;
+      uint32_t xs[4] = {0, 0, 0, 0}, gd[4] = {0, 0, 0, 0};
+      for (;;) {
+        // a lane whose entry is used up takes its next one (an entry's mask
+        // may be empty: the stream's first positions are no anchors)
+        while (!mask && i != kNoEntry) {
+          const uint32_t e0 = wl.e[2 * i];
+          rel = ((e0 >> 8) & 0xFFu) << 4;
+          mask = e0 >> 16;
+          const uint4 v = wl.x[i];
+          xs[0] = v.x;
+          xs[1] = v.y;
+          xs[2] = v.z;
+          xs[3] = v.w;
+          // the gear before each dword of the piece
+          gd[0] = wl.e[2 * i + 1];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) gd[d + 1] = (gd[d] << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
-        uint32_t& k = rel < kHalfSpan ? k_lo : k_hi;
-        k -= __popc(mask);
-        for (uint32_t w = k; mask; mask &= mask - 1, ++w) {
+          for (int d = 0; d < 3; ++d) gd[d + 1] = (gd[d] << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
+          uint32_t& k = rel < kHalfSpan ? k_lo : k_hi;
+          k -= __popc(mask);
+          w = k;
+          i = e0 & 0xFFu;
+        }
+        if (__ballot(mask != 0) == 0) break;
+        if (ABL & ABL_TE_NO_ANCHOR_STORE) {
+          mask = 0;
+          continue;
+        }
+        if (mask) {
           const uint32_t t = __builtin_ctz(mask), d = t >> 2, q = t & 3u;
           const uint32_t gdd = d == 0 ? gd[0] : d == 1 ? gd[1] : d == 2 ? gd[2] : gd[3];
           const uint32_t xd = d == 0 ? xs[0] : d == 1 ? xs[1] : d == 2 ? xs[2] : xs[3];
@@ -595,8 +627,10 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
           const uint32_t g = (gdd << (q + 1)) + __builtin_amdgcn_udot4(xd, 0x01020408u >> (8 * (3 - q)), 0u, false);
           po.rel[base + w] = sbase + rel + t;
           po.g[base + w] = g;
+          mask &= mask - 1;
+          ++w;
         }
-        i = e0 & 0xFFu;
+        nst += 2;
       }
     }
   }
@@ -605,7 +639,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
     po.cnt[wt] = over ? ZC_WT_OVERFLOW : tot;
     if (!(ABL & ABL_NO_ATOMIC)) atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
   }
-  return kDigests / 2 + 2 + ((ABL & ABL_NO_ATOMIC) ? 0 : 1);
+  return kDigests / 2 + __builtin_amdgcn_readfirstlane(nst) + 2 + ((ABL & ABL_NO_ATOMIC) ? 0 : 1);
 }
 
 // The workgroup's rounds form one flat sequence over its tiles (32 per
@@ -639,12 +673,13 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   }
   const uint32_t sw = row_swizzle(lane);  // read-side swizzle of this lane's row
   const uint32_t hs = (lane & 1) * kHalfRounds;  // logical round r is physical round r ^ hs
-  v4u32 warm[2];                          // the 32 bytes before the next half span
+  v4u32 warm[2] = {};                       // the 32 bytes before the next half span
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kRpt, r = Rx - k * kRpt;
     const uint64_t tile = tile0 + blockIdx.x + (uint64_t)k * grid;
-    stage_round(data, myring, wave, lane_off, tile, (int)r, Rx & 1);
-    if (r % kHalfRounds == 0) {
+    stage_round<((ABL & ABL_DMA_NT) ? 2 : 0) | ((ABL & ABL_DMA_SC1) ? 16 : 0)>(data, myring, wave, lane_off, tile,
+                                                                                  (int)r, Rx & 1);
+    if (!(ABL & ABL_NO_WARM) && r % kHalfRounds == 0) {
       // span 0 of the stream has no bytes before it: it reads itself (unused)
       const uint64_t at = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN + (uint64_t)(r ^ hs) * ZC_ROUND;
       const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
@@ -652,6 +687,12 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       warm[1] = global_read16(src + 16);
     }
   };
+  if (ABL & (ABL_STAGGER_HALF | ABL_STAGGER_QUARTER)) {
+    // ablation: odd waves start later, so a SIMD's two waves reach their
+    // tile ends at different times
+    if (wave & 1)
+      for (int i = 0; i < ((ABL & ABL_STAGGER_HALF) ? 14 : 7); ++i) __builtin_amdgcn_s_sleep(127);
+  }
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
   ScanLane s{0, 0, 0};
@@ -671,7 +712,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     // plus the next half's warm-up loads before a half's first round, plus
     // the tile end's stores before round 0
     if (R + 1 >= nR) wait_vmcnt<0>();
-    else if ((r + 1) % kHalfRounds == 0) wait_vmcnt<kDmaRound + 2>();
+    else if ((r + 1) % kHalfRounds == 0) wait_vmcnt<(ABL & ABL_NO_WARM) ? kDmaRound : kDmaRound + 2>();
     else if (r == 0) wait_vmcnt_dyn(kDmaRound + tail_stores);
     else wait_vmcnt<kDmaRound>();
     const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND);
@@ -688,7 +729,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       // 32 bytes before only, so this equals the gear rolled on continuously)
       s.glo = 0;
       ties(warm);  // landed: the wait above covers them
-      if (span0 + pr * ZC_ROUND >= 64) {
+      if (!(ABL & ABL_NO_WARM) && span0 + pr * ZC_ROUND >= 64) {
         const uint32_t xs[8] = {warm[0][0], warm[0][1], warm[0][2], warm[0][3],
                                 warm[1][0], warm[1][1], warm[1][2], warm[1][3]};
 #pragma unroll
@@ -2244,7 +2285,7 @@ hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, ui
                              uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
   if (!ntiles) return hipSuccess;
   const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
-  hipLaunchKernelGGL(zc_scan_kernel<0>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles, anchor_lo, blk,
+  hipLaunchKernelGGL(zc_scan_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles, anchor_lo, blk,
                      po, counters);
   return hipGetLastError();
 }
