@@ -376,11 +376,14 @@ def run_rank(args):
         t1 = time.perf_counter()
         nrec_feed = 0
         pos = 0
+        copy_s = 0.0
         while pos < n:
             dst = b4._L.zc_get_input_buffer(b4._ctx)
             room = b4.get_input_buffer_size()
             m = min(room, n - pos)
+            tc = time.perf_counter()
             ctypes.memmove(dst, src + pos, m)
+            copy_s += time.perf_counter() - tc
             b4.handle_more_data(m)
             pos += m
             nrec_feed += len(b4.take_records())
@@ -393,7 +396,8 @@ def run_rank(args):
                           "path": "getInputBuffer/handleMoreData through the default bounded window "
                                   f"({fst['window_bytes'] >> 20} MiB), a host memcpy per piece standing for "
                                   "fread, records taken as they are cut",
-                          "records": nrec_feed, "segments": fst["segments"], "hbm_bytes": fst["hbm_bytes"]}
+                          "records": nrec_feed, "segments": fst["segments"], "hbm_bytes": fst["hbm_bytes"],
+                          "host_memcpy_s": round(copy_s, 4), "feed_s": round(feed_s, 4)}
         del host
 
     cpu = None
