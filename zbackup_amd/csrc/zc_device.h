@@ -118,11 +118,31 @@ inline uint32_t bloom_bits_for(size_t keys) {
   while (b < 24 && ((size_t)(keys > (512u << 10) ? 1 : 2) << b) < keys) ++b;
   return b;
 }
+// The Bloom buffer: 2^bits blocks of two words, then a 2^19-bit first level
+// (one bit per key, from the high word of key * golden) that the staged
+// screen holds in LDS: positions whose bit is clear skip the block gather
+constexpr uint32_t kBloomPfBits = 19;
+constexpr uint32_t kBloomPfWords = 1u << (kBloomPfBits - 5);
+inline size_t bloom_words(uint32_t bits) { return ((size_t)2 << bits) + kBloomPfWords; }
+__host__ __device__ inline uint32_t bloom_pf(uint64_t key) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & ((1u << kBloomPfBits) - 1u);
+}
 __host__ __device__ inline uint32_t bloom_block(uint64_t key, uint32_t bits) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));
 }
+// the six bit positions of a key in its block: 5-bit fields of one 32-bit
+// mix of both key words (two VALU ops; the block index and the first level
+// come from key * golden)
 __host__ __device__ inline uint32_t bloom_seed(uint64_t key) {
-  return (uint32_t)(((key ^ (key >> 31)) * 0xBF58476D1CE4E5B9ull) >> 32);
+  return ((uint32_t)key ^ (uint32_t)(key >> 32)) * 0x85EBCA6Bu;
+}
+// all six bits of seed g set in block word pair (x, y)?  Shifts by the
+// 5-bit fields: the hardware shift takes its amount mod 32, so each field
+// costs one shift (and one more to move it down)
+__host__ __device__ inline uint32_t bloom_test(uint32_t x, uint32_t y, uint32_t g) {
+  const uint32_t tx = (x >> (g & 31u)) & (x >> ((g >> 5) & 31u)) & (x >> ((g >> 10) & 31u));
+  const uint32_t ty = (y >> ((g >> 15) & 31u)) & (y >> ((g >> 20) & 31u)) & (y >> ((g >> 25) & 31u));
+  return tx & ty & 1u;
 }
 __host__ __device__ inline uint32_t bloom_lo(uint32_t g) {
   return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)) | (1u << ((g >> 10) & 31u));

@@ -402,7 +402,8 @@ void statics_screen(zc_ctx& c) {
   for (const auto& kv : c.smap) keys.push_back(kv.first);
   c.sc_fbits.assign(1u << 14, 0);
   c.bloom_bits = bloom_bits_for(keys.size() + 64);
-  std::vector<uint32_t> bloom(2u << c.bloom_bits, 0);
+  std::vector<uint32_t> bloom(bloom_words(c.bloom_bits), 0);
+  uint32_t* const pf = bloom.data() + (2u << c.bloom_bits);
   uint32_t bits = 10;
   while ((1ull << bits) < 2ull * keys.size() + 2) ++bits;
   std::vector<uint64_t> set(1ull << bits, 0);
@@ -413,6 +414,8 @@ void statics_screen(zc_ctx& c) {
     const uint32_t b = bloom_block(k, c.bloom_bits), g = bloom_seed(k);
     bloom[2 * b] |= bloom_lo(g);
     bloom[2 * b + 1] |= bloom_hi(g);
+    const uint32_t f = bloom_pf(k);
+    pf[f >> 5] |= 1u << (f & 31);
     if (k == 0) {
       c.kset_zero = 1;
       continue;
@@ -1283,8 +1286,8 @@ class Resolver {
       h2d(c_, c_.flist.p, fk.data(), fk.size());
       flist_n_ = (uint32_t)fk.size();
       if (!fk.empty()) {  // the epoch's keys join a copy of the set's filter
-        c_.bloom_w.ensure(2u << c_.bloom_bits);
-        HCK(hipMemcpyAsync(c_.bloom_w.p, c_.bloom_s.p, (2 * sizeof(uint32_t)) << c_.bloom_bits,
+        c_.bloom_w.ensure(bloom_words(c_.bloom_bits));
+        HCK(hipMemcpyAsync(c_.bloom_w.p, c_.bloom_s.p, sizeof(uint32_t) * bloom_words(c_.bloom_bits),
                            hipMemcpyDeviceToDevice, c_.stream));
         HCK(launch_bloom_add(c_.bloom_w.p, c_.bloom_bits, c_.flist.p, (uint32_t)fk.size(), c_.stream));
         bloom_p_ = c_.bloom_w.p;

@@ -1614,6 +1614,10 @@ struct FKeys {
 // per position) need more than the exact modes' two
 template <int NF>
 constexpr int kFRS = NF == 64 ? 7 : kFRunSlots;
+// threads per workgroup: the Bloom mode runs 4 waves (one per SIMD; the
+// filter gathers, not latency, bound it) so the LDS holds its first level
+template <int NF>
+constexpr int kFTPBn = NF == 64 ? 256 : ZC_FTPB;
 
 template <int RS>
 __device__ __forceinline__ void put_run(uint32_t (&rs)[RS], uint32_t (&re)[RS], uint32_t i, uint32_t a, uint32_t b) {
@@ -1687,24 +1691,31 @@ __device__ __forceinline__ uint4 funnel16(uint4 lo, uint4 hi, uint32_t s) {
 }
 
 template <int Q, int NF>
-__global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
+__global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
     const uint8_t* __restrict__ data, uint64_t n, const uint64_t* __restrict__ blk, uint32_t W, uint32_t pw32,
     uint32_t sbyte, uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt, FKeys K,
     const uint32_t* __restrict__ fmap,
     Run* __restrict__ runs, uint64_t runs_cap, uint64_t* __restrict__ wt_off, uint32_t* __restrict__ wt_cnt,
     unsigned long long* __restrict__ counters) {
-  constexpr int kWaves = ZC_FTPB / 64;
+  constexpr int kTPB = kFTPBn<NF>;
+  constexpr int kWaves = kTPB / 64;
   constexpr uint32_t kSlot = 64 * ZC_FROUND;  // bytes of one stream's round
   __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves][2][2 * kSlot];  // [slot][in | out]
   __shared__ uint32_t s_map[NF == 0 || NF == 16 || NF == 32 ? kFMapWords : 1];
   __shared__ uint32_t s_keys[NF == 32 ? kFLdsKeys : 1];
+  __shared__ uint32_t s_pf[NF == 64 ? kBloomPfWords : 1];  // the Bloom filter's first level
   constexpr int RS = kFRS<NF>;
   __shared__ uint32_t s_rs[kWaves][64 * RS], s_re[kWaves][64 * RS];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (NF == 0 || NF == 16 || NF == 32) {
-    for (uint32_t i = tid; i < kFMapWords; i += ZC_FTPB) s_map[i] = fmap[i];
+    for (uint32_t i = tid; i < kFMapWords; i += kTPB) s_map[i] = fmap[i];
     if (NF == 32)
-      for (uint32_t i = tid; i < K.nk; i += ZC_FTPB) s_keys[i] = K.dkeys[i];
+      for (uint32_t i = tid; i < K.nk; i += kTPB) s_keys[i] = K.dkeys[i];
+    __syncthreads();
+  }
+  if (NF == 64) {
+    const uint4* pf = (const uint4*)(K.bloom + (2u << K.nk));
+    for (uint32_t i = tid; i < kBloomPfWords / 4; i += kTPB) ((uint4*)s_pf)[i] = pf[i];
     __syncthreads();
   }
   const uint32_t m = (uint32_t)(4 * Q) + sbyte;  // = -W mod 16
@@ -1842,35 +1853,49 @@ __global__ void __launch_bounds__(ZC_FTPB, 1) zc_fscan_staged_kernel(
           }
         }
       }
-      // two halves of two pieces: 32 gathers in flight per lane each
+      // two halves of two pieces: 32 gathers in flight per lane each.  A
+      // position first tests the filter's first level in LDS; one whose bit
+      // is clear gathers block 0 instead of its own (all such lanes of the
+      // wave share one line), so the L2 gathers scale with the first level's
+      // fill, not with the positions
       const uint2* const bl = (const uint2*)K.bloom;
+      const uint32_t bsh = 32u - K.nk;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         uint2 bw[2][16];
-        uint32_t gs[2][16];
+        uint32_t gs[2][16], pre[2];
 #pragma unroll
         for (int pi = 0; pi < 2; ++pi) {
           const int p = 2 * hf + pi;
           const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
+          uint32_t bi[16], pw[16];
 #pragma unroll
           for (int d = 0; d < 4; ++d)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xo[p][d] >> (8 * q)) & 0xFFu) * K.pw64;
               const uint64_t key = V64 + K.pw64;
-              bw[pi][4 * d + q] = bl[bloom_block(key, K.nk)];
+              // bloom_block and bloom_pf: the high word of key * golden
+              const uint32_t hi = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32);
+              const uint32_t f = hi & ((1u << kBloomPfBits) - 1u);
+              bi[4 * d + q] = hi >> bsh;
+              pw[4 * d + q] = s_pf[f >> 5] >> (f & 31u);
               gs[pi][4 * d + q] = bloom_seed(key);
             }
+          uint32_t pm = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            pm |= (pw[i] & 1u) << i;
+            bw[pi][i] = bl[(pw[i] & 1u) ? bi[i] : 0u];
+          }
+          pre[pi] = pm;
         }
 #pragma unroll
         for (int pi = 0; pi < 2; ++pi) {
           uint32_t m16 = 0;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const uint32_t ml = bloom_lo(gs[pi][i]), mh = bloom_hi(gs[pi][i]);
-            m16 |= ((bw[pi][i].x & ml) == ml && (bw[pi][i].y & mh) == mh ? 1u : 0u) << i;
-          }
-          hm[2 * hf + pi] = m16;
+          for (int i = 0; i < 16; ++i) m16 |= bloom_test(bw[pi][i].x, bw[pi][i].y, gs[pi][i]) << i;
+          hm[2 * hf + pi] = m16 & pre[pi];
         }
       }
       if (R + 2 < nR) issue(R + 2);
@@ -2054,6 +2079,8 @@ __global__ void zc_bloom_add_kernel(uint32_t* __restrict__ bloom, uint32_t bits,
   const uint32_t b = bloom_block(keys[i], bits), g = bloom_seed(keys[i]);
   atomicOr(&bloom[2 * b], bloom_lo(g));
   atomicOr(&bloom[2 * b + 1], bloom_hi(g));
+  const uint32_t f = bloom_pf(keys[i]);
+  atomicOr(&bloom[(2u << bits) + (f >> 5)], 1u << (f & 31));
 }
 
 // 64-bit key sets of the screen's run filter: open addressing (empty = 0),
@@ -2438,7 +2465,7 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
                                         Run* runs, uint64_t runs_cap, uint64_t* wt_off, uint32_t* wt_cnt,
                                         unsigned long long* counters) {
 #define ZC_FS(NF)                                                                                                  \
-  hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(ZC_FTPB), 0, s, data, n, blk, W, pw32,     \
+  hipLaunchKernelGGL((zc_fscan_staged_kernel<Q, NF>), dim3(grid), dim3(kFTPBn<NF>), 0, s, data, n, blk, W, pw32, \
                      sbyte, p_start, p_end, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
   if (nfk == 1) ZC_FS(1);
   else if (nfk == 64) ZC_FS(64);
@@ -2488,8 +2515,9 @@ hipError_t launch_fscan_staged_bloom(const uint8_t* data, uint64_t n, const uint
   K.nk = bloom_bits;
   K.pw64 = pow257_dev(W);
   const uint32_t m = (16u - W % 16u) % 16u;
-  const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * (ZC_FTPB / 64));
-  const unsigned grid = (waves + ZC_FTPB / 64 - 1) / (ZC_FTPB / 64);
+  constexpr unsigned kW64 = kFTPBn<64> / 64;
+  const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * kW64);
+  const unsigned grid = (waves + kW64 - 1) / kW64;
   switch (m >> 2) {
     case 0: return launch_fscan_staged_q<0>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                             nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
