@@ -343,6 +343,34 @@ def run_rank(args):
             b2.close()
             extras["value_sha1"] = job_value(n, world, args.sha1_steps, el2)
             extras["sha1_ms_per_step"] = el2 / args.sha1_steps * 1e3
+        # incremental backups on one context: with SHA-1 ids a stream's chunks
+        # stay in the context's index (Writer::add -> ChunkIndex::addChunk), so
+        # a later stream is matched against them through the historic index --
+        # the same 8 GiB again (every chunk a duplicate), and the stream after a
+        # different 8 GiB one (131,072 historic entries, none matching)
+        if not args.sha1:
+            other = torch.empty(n, dtype=torch.uint8, device=buf.device)
+            fill_stream(torch, other, n, args.config, seed + 1000003, local)
+            inc = {}
+            for label, first in (("same_stream_again", buf), ("after_other_stream", other)):
+                b5 = BackupCreator(W64, device=local, sha1=True, timing=True)
+                b5.chunk_device(first.data_ptr(), n)
+                torch.cuda.synchronize()
+                reps = 3 if label == "same_stream_again" else 1
+                ts = []
+                for _ in range(reps):
+                    t1 = time.perf_counter()
+                    b5.chunk_device(buf.data_ptr(), n)
+                    torch.cuda.synchronize()
+                    ts.append(time.perf_counter() - t1)
+                st5 = b5.stats()
+                kinds = b5.records()["kind"]
+                b5.close()
+                inc[label] = {"value": round(job_value(n, world, 1, job_max(min(ts), world)), 3), "unit": "GiB/s",
+                              "ms": round(min(ts) * 1e3, 3), "dup_records": int((kinds == 1).sum()),
+                              "new_records": int((kinds == 0).sum()), "hist_entries": st5["hist_entries"]}
+            del other
+            extras["incremental"] = inc
         # the stream starts in (pinned) host memory, as in zutils.cc:100-124
         host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
         host.copy_(buf)
@@ -462,6 +490,8 @@ def run_rank(args):
             e["value"] = round(e["value"], 3)
             e["ms_per_step"] = round(e["ms_per_step"], 3)
             out["end_to_end"] = e
+        if "incremental" in extras:
+            out["incremental_sha1"] = extras["incremental"]
         if "feed" in extras:
             f = extras["feed"]
             f["value"] = round(f["value"], 3)

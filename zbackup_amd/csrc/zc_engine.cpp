@@ -1151,6 +1151,13 @@ class Resolver {
       std::vector<size_t> sidx;
       for (size_t j = 0; j < hidx.size(); ++j)
         if (key[j] == c_.hkey[hc[hidx[j]].ref]) {
+          // a window that is a grid chunk has its SHA-1 from the speculative
+          // grid pass (the incremental backup of unchanged data: all of them)
+          if (const uint8_t* g = grid_sha_of(ha[j])) {
+            const uint64_t i = hidx[j];
+            if (memcmp(g, &c_.hsha[16 * (size_t)hc[i].ref], 16) == 0) hcands_.push_back({hc[i].p, hc[i].ref});
+            continue;
+          }
           sa.push_back(ha[j]);
           sl.push_back(W_);
           sidx.push_back(j);
@@ -1977,8 +1984,29 @@ class Resolver {
   // SHA-1 kernel needs no LDS, so it shares the CUs with the scan's
   // workgroups); finalize() takes every record that is one of them from there
   uint64_t pre_sha_n_ = 0;
+  std::vector<uint8_t> gsha_h_;  // the grid chunks' SHA-1 on the host, once needed
+  bool gsha_ready_ = false;
+  const uint8_t* grid_sha() {
+    if (!gsha_ready_) {
+      gsha_h_.resize(pre_sha_n_ * 20);
+      if (pre_sha_n_) {
+        HCK(hipMemcpyAsync(gsha_h_.data(), c_.gsha.p, gsha_h_.size(), hipMemcpyDeviceToHost, c_.sha_stream));
+        HCK(hipStreamSynchronize(c_.sha_stream));
+      }
+      gsha_ready_ = true;
+    }
+    return gsha_h_.data();
+  }
+  // grid chunk q's SHA-1 when window [ws, ws + W) is that chunk, else null
+  const uint8_t* grid_sha_of(uint64_t ws) {
+    if (!pre_sha_n_ || ws % W_) return nullptr;
+    const uint64_t q = ws / W_;
+    if (q >= pre_sha_n_ || ws + W_ > n_) return nullptr;
+    return grid_sha() + 20 * q;
+  }
   void pre_sha() {
     pre_sha_n_ = 0;
+    gsha_ready_ = false;
     if (!(c_.flags & ZC_FLAG_SHA1) || !indexable_ || n_ < W_) return;
     const uint64_t k = (n_ + W_ - 1) / W_;
     if (k > 0xFFFFFFFFull) return;
@@ -2019,12 +2047,7 @@ class Resolver {
     need_digest_.clear();
     const size_t r0 = c_.nrec_done;
     if (c_.flags & ZC_FLAG_SHA1) {
-      std::vector<uint8_t> gsha;
-      if (pre_sha_n_) {
-        gsha.resize(pre_sha_n_ * 20);
-        HCK(hipMemcpyAsync(gsha.data(), c_.gsha.p, gsha.size(), hipMemcpyDeviceToHost, c_.sha_stream));
-        HCK(hipStreamSynchronize(c_.sha_stream));
-      }
+      const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;
       std::vector<uint64_t> sa;
       std::vector<uint32_t> sl;
       std::vector<size_t> idx;
