@@ -72,3 +72,25 @@ def test_large_static_index_window_vs_oracle(torch_cuda):
         bc.feed(data)
         bc.finish()
         _same(bc.records(), want)
+
+
+@pytest.mark.parametrize("W", [1000, 4099, 300007])
+def test_bloom_screen_odd_w_vs_oracle(torch_cuda, W):
+    """The Bloom mode of the staged screen (over 2048 by-value keys) at chunk
+    sizes whose out-byte funnel shifts differ (-W mod 16 = 8, 13, 9), on a
+    stream long enough (> 64 MiB) for the staged kernel to run."""
+    from zbackup_amd import BackupCreator
+    old = oracle.gen("R9:8000000")
+    real = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(old, W) if k == "N" and s == W][:400]
+    zero = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(oracle.gen(f"Z:{W}"), W)]
+    rng = np.random.default_rng(W)
+    keys = rng.integers(1, 2**63, 3000, dtype=np.int64)
+    shas = rng.integers(0, 256, (3000, 16), dtype=np.uint8)
+    seeds = real + zero + [(shas[i].tobytes(), int(keys[i]), W) for i in range(3000)]
+    data = oracle.gen("R5:40000000,R9:8000000,Z:1000000,R6:30000000,C41000000:3000000")
+    want = oracle.chunk_array(data, W, seeds=seeds)
+    assert (want["kind"] == 1).sum() >= len(real)
+    t = torch_cuda.from_numpy(data).to("cuda")
+    with BackupCreator(W, seeds=seeds, sha1=True) as bc:
+        bc.chunk_device(t.data_ptr(), data.size)
+        _same(bc.records(), want)
