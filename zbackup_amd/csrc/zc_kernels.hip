@@ -1151,7 +1151,8 @@ __device__ __forceinline__ bool wave_ranges_equal(const uint8_t* __restrict__ da
     uint4 x[8], y[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      __builtin_memcpy(&x[k], data + a + i + k * 1024, 16);
+      const v4u32 xv = __builtin_nontemporal_load((const v4u32*)(data + a + i + k * 1024));  // read once
+      x[k] = make_uint4(xv[0], xv[1], xv[2], xv[3]);
       __builtin_memcpy(&y[k], data + b + i + k * 1024, 16);
     }
 #pragma unroll
@@ -1189,7 +1190,10 @@ __device__ __forceinline__ bool wave_ranges_equal_rot(const uint8_t* __restrict_
       uint32_t bk = blk0 + t + k;
       bk = bk >= nb ? bk - nb : bk;
       const uint32_t i = bk * 1024 + lane * 16;
-      __builtin_memcpy(&x[k], data + a + i, 16);
+      // the member side is read once: non-temporal (whole lines, 1 KiB per
+      // instruction); the leader side may be shared by many members (C5)
+      const v4u32 xv = __builtin_nontemporal_load((const v4u32*)(data + a + i));
+      x[k] = make_uint4(xv[0], xv[1], xv[2], xv[3]);
       __builtin_memcpy(&y[k], data + b + i, 16);
     }
 #pragma unroll
