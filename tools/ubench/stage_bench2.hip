@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(TPB, 1) stage_kernel(const uint8_t* __restrict
       const uint32_t p = (lane % PIECES) ^ swz(row);
       const uint64_t wbase = tile * (uint64_t)(TPB * S) + (uint64_t)wave * 64 * S;
       const uint64_t off = CONTIG ? (uint64_t)r * 64 * ROWB + (uint64_t)row * ROWB : (uint64_t)row * S + ((r * ROWB + ((wave * 64 + row) % ROT) * (S / ROT)) % S);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wbase + off + p * 16), (lds_void_t*)(slot + j * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(data + wbase + off + p * 16), (lds_void_t*)(slot + j * 1024), 16, 0, 2);  // nt, as the product
     }
   };
   for (uint64_t R = 0; R < nR && R < SLOTS; ++R) issue(R);
