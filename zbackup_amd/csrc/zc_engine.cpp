@@ -32,6 +32,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -185,6 +186,10 @@ struct DefaultInit : std::allocator<T> {
 // A few host threads for the record writing of long grid runs (a stream's
 // records are ~40 bytes each, 131,072 per 8 GiB: one core writes them at its
 // store bandwidth).  Workers sleep between jobs; the caller takes a share.
+static_assert(sizeof(zc_record) == 40 && offsetof(zc_record, size) == 8 && offsetof(zc_record, kind) == 12 &&
+                  offsetof(zc_record, rolling) == 16 && offsetof(zc_record, sha1) == 24,
+              "the streamed record writes assume this layout");
+
 class HostPool {
  public:
   static HostPool& get() {
@@ -1733,14 +1738,31 @@ class Resolver {
       const uint64_t* key = c_.h_key.p;
       zc_record* out = rec + o;
       HostPool::get().run(kmax - ks_, [&](size_t a, size_t b) {
-        for (size_t j = a; j < b; ++j) {
+        auto put = [&](size_t j) {
           zc_record& r = out[j];
           r.offset = r0 + (k0 + j) * W;
           r.size = W;
           r.kind = kind;
           r.rolling = idx ? key[k0 + j] : 0;
           memset(r.sha1, 0, sizeof r.sha1);
+        };
+        // two 40-byte records are five 16-byte words: streamed past the
+        // caches (no read-for-ownership of the lines they overwrite)
+        size_t j = a;
+        for (; j < b && ((uintptr_t)(out + j) & 15); ++j) put(j);
+        for (; j + 2 <= b; j += 2) {
+          const uint64_t o0 = r0 + (k0 + j) * W, o1 = o0 + W;
+          const uint64_t h0 = idx ? key[k0 + j] : 0, h1 = idx ? key[k0 + j + 1] : 0;
+          const uint64_t sk = (uint64_t)W | ((uint64_t)kind << 32);
+          __m128i* d = (__m128i*)(out + j);
+          _mm_stream_si128(d + 0, _mm_set_epi64x((long long)sk, (long long)o0));
+          _mm_stream_si128(d + 1, _mm_set_epi64x(0, (long long)h0));
+          _mm_stream_si128(d + 2, _mm_set_epi64x((long long)o1, 0));
+          _mm_stream_si128(d + 3, _mm_set_epi64x((long long)h1, (long long)sk));
+          _mm_stream_si128(d + 4, _mm_setzero_si128());
         }
+        for (; j < b; ++j) put(j);
+        _mm_sfence();
       });
       s_ = r_e_ + kmax * W_;
       ks_ = kmax;
