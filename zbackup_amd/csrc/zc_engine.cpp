@@ -265,6 +265,42 @@ class HostPool {
   bool stop_ = false;
 };
 
+// records of grid chunks k0 .. k0 + n - 1 of an epoch at r0 (offset r0 + k W,
+// size W, one kind, rolling hash key[k] or 0), in parallel when many: two
+// 40-byte records are five 16-byte words, streamed past the caches (no
+// read-for-ownership of the lines they overwrite)
+constexpr uint64_t kParallelRecordsMin = 32768;
+void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uint32_t W, uint32_t kind,
+                       const uint64_t* key) {
+  auto fill = [&](size_t a, size_t b) {
+    auto put = [&](size_t j) {
+      zc_record& r = out[j];
+      r.offset = r0 + (k0 + j) * W;
+      r.size = W;
+      r.kind = kind;
+      r.rolling = key ? key[k0 + j] : 0;
+      memset(r.sha1, 0, sizeof r.sha1);
+    };
+    size_t j = a;
+    for (; j < b && ((uintptr_t)(out + j) & 15); ++j) put(j);
+    const uint64_t sk = (uint64_t)W | ((uint64_t)kind << 32);
+    for (; j + 2 <= b; j += 2) {
+      const uint64_t o0 = r0 + (k0 + j) * W, o1 = o0 + W;
+      const uint64_t h0 = key ? key[k0 + j] : 0, h1 = key ? key[k0 + j + 1] : 0;
+      __m128i* d = (__m128i*)(out + j);
+      _mm_stream_si128(d + 0, _mm_set_epi64x((long long)sk, (long long)o0));
+      _mm_stream_si128(d + 1, _mm_set_epi64x(0, (long long)h0));
+      _mm_stream_si128(d + 2, _mm_set_epi64x((long long)o1, 0));
+      _mm_stream_si128(d + 3, _mm_set_epi64x((long long)h1, (long long)sk));
+      _mm_stream_si128(d + 4, _mm_setzero_si128());
+    }
+    for (; j < b; ++j) put(j);
+    _mm_sfence();
+  };
+  if (n >= kParallelRecordsMin) HostPool::get().run(n, fill);
+  else fill(0, n);
+}
+
 class Resolver;
 
 }  // namespace
@@ -1732,38 +1768,7 @@ class Resolver {
     const uint8_t* dead = indexable_ ? dead_.data() + nconf_ : nullptr;
     if (ndead_ == 0 && r_e_ + ks_ * W_ >= s_ && kmax - ks_ >= kParallelRecords) {
       // every chunk of the run is saved: record o + j is grid chunk ks_ + j
-      const uint64_t k0 = ks_, r0 = r_e_;
-      const uint32_t W = W_;
-      const bool idx = indexable_;
-      const uint64_t* key = c_.h_key.p;
-      zc_record* out = rec + o;
-      HostPool::get().run(kmax - ks_, [&](size_t a, size_t b) {
-        auto put = [&](size_t j) {
-          zc_record& r = out[j];
-          r.offset = r0 + (k0 + j) * W;
-          r.size = W;
-          r.kind = kind;
-          r.rolling = idx ? key[k0 + j] : 0;
-          memset(r.sha1, 0, sizeof r.sha1);
-        };
-        // two 40-byte records are five 16-byte words: streamed past the
-        // caches (no read-for-ownership of the lines they overwrite)
-        size_t j = a;
-        for (; j < b && ((uintptr_t)(out + j) & 15); ++j) put(j);
-        for (; j + 2 <= b; j += 2) {
-          const uint64_t o0 = r0 + (k0 + j) * W, o1 = o0 + W;
-          const uint64_t h0 = idx ? key[k0 + j] : 0, h1 = idx ? key[k0 + j + 1] : 0;
-          const uint64_t sk = (uint64_t)W | ((uint64_t)kind << 32);
-          __m128i* d = (__m128i*)(out + j);
-          _mm_stream_si128(d + 0, _mm_set_epi64x((long long)sk, (long long)o0));
-          _mm_stream_si128(d + 1, _mm_set_epi64x(0, (long long)h0));
-          _mm_stream_si128(d + 2, _mm_set_epi64x((long long)o1, 0));
-          _mm_stream_si128(d + 3, _mm_set_epi64x((long long)h1, (long long)sk));
-          _mm_stream_si128(d + 4, _mm_setzero_si128());
-        }
-        for (; j < b; ++j) put(j);
-        _mm_sfence();
-      });
+      fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr);
       s_ = r_e_ + kmax * W_;
       ks_ = kmax;
       return;
@@ -1825,22 +1830,7 @@ class Resolver {
     if (!nchain) return;
     const size_t o = c_.recs.size();
     c_.recs.resize(o + nchain);
-    zc_record* out = c_.recs.data() + o;
-    const uint64_t k0 = j + 1, r0 = r_e_;
-    const uint32_t W = W_;
-    const uint64_t* key = c_.h_key.p;
-    auto fill = [&](size_t a, size_t b) {
-      for (size_t i = a; i < b; ++i) {
-        zc_record& r = out[i];
-        r.offset = r0 + (k0 + i) * W;
-        r.size = W;
-        r.kind = ZC_CHUNK_DUP;
-        r.rolling = key[k0 + i];
-        memset(r.sha1, 0, sizeof r.sha1);
-      }
-    };
-    if (nchain >= kParallelRecords) HostPool::get().run(nchain, fill);
-    else fill(0, nchain);
+    fill_grid_records(c_.recs.data() + o, nchain, r_e_, j + 1, W_, ZC_CHUNK_DUP, c_.h_key.p);
     r_ = r_e_ + (uint64_t)jn * W_;
     s_ = r_;
     if (jn > ks_) ks_ = jn;
