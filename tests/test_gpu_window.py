@@ -163,3 +163,26 @@ def test_unbounded_window_still_works(torch_cuda):
         bc.feed(data)
         bc.finish()
         _same(bc.records(), want)
+
+
+@pytest.mark.parametrize("W,block,piece", [(65536, 48 << 20, 1 << 20), (4096, 24 << 20, 64 << 10)])
+def test_window_edited_duplicate_vs_oracle(torch_cuda, W, block, piece):
+    """An edited duplicate (a block, then the block with 1-100 random bytes
+    inserted every `piece` bytes: one grid shift per insertion, walked lazily
+    on the shifted grid) fed through the smallest window: the lazy-shift state
+    crosses window segments and slides."""
+    from zbackup_amd import BackupCreator
+    rng = np.random.default_rng(W + 1)
+    segs, off = [f"R77:{block}"], 0
+    while off < block:
+        ln = min(piece, block - off)
+        segs += [f"C{off}:{ln}", f"R{int(rng.integers(1, 1 << 30))}:{int(rng.integers(1, 101))}"]
+        off += ln
+    data = oracle.gen(",".join(segs))
+    want = oracle.chunk_array(data, W)
+    assert (want["kind"] == 1).sum() > block // W // 2
+    with BackupCreator(W, sha1=True, window=1) as bc:
+        got, _ = _feed(bc, data, np.random.default_rng(3), 5 << 20)
+        st = bc.stats()
+    assert st["segments"] >= 4
+    _same(got, want)
