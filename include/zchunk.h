@@ -178,6 +178,31 @@ int zc_sha256_finish(zc_sha256* h, uint8_t out[32]);             /* Sha256::fini
 int zc_sha256_destroy(zc_sha256* h);
 int zc_sha256_impl(const zc_sha256* h); /* 1: x86 SHA extensions, 0: scalar */
 
+/* ---- Bundle writer offload ----
+ * ChunkStorage::Writer::add's bundling rule (chunk_storage.cc:31-46): the chunks that
+ * index.addChunk accepted, in order; chunk i joins the current bundle unless the bundle's
+ * payload + sizes[i] > max_payload (config bundle.max_payload_size, default 0x200000,
+ * zbackup.proto:88), which first finishes the bundle.  bundle_of[i] receives chunk i's
+ * bundle, *n_bundles their count.  Host bookkeeping only (no device work). */
+int zc_bundle_plan(const uint64_t* sizes, size_t n, uint64_t max_payload, uint32_t* bundle_of,
+                   size_t* n_bundles);
+/* Bundle::Creator::addChunk's payload (bundle.cc:30-36) on the device: chunk i's bytes
+ * d_src[src_off[i] ..+ sizes[i]) appended to d_payload back to back (HBM to HBM). */
+int zc_bundle_gather(zc_ctx* ctx, const void* d_src, const uint64_t* src_off, const uint64_t* sizes,
+                     size_t n, void* d_payload);
+/* The lzo1x_1 compression Bundle::Creator::write runs on each bundle's payload
+ * (bundle.cc:120-151 -> LZO1X_1_Encoder::doProcessNoSize, compression.cc:586-606 -> liblzo2
+ * lzo1x_1_compress) with zbackup's framing (NoStreamAndUnknownSizeEncoder::doProcess,
+ * compression.cc:435-466: LE32 size, "EFGH", LE32 compressed size, "MNOP", the LZO stream):
+ * payload i = d_payload[pay_off[i] ..+ pay_size[i]) (pay_size[i] < 2^32), its framed bytes go
+ * to d_out + out_off[i], which must leave zc_lzo_capacity(pay_size[i]) bytes; out_size[i]
+ * (host) receives their count.  The bytes equal what the reference writes for the payload. */
+uint64_t zc_lzo_capacity(uint64_t payload_size); /* LZO1X_1_Encoder::suggestOutputSize + 16 */
+int zc_lzo_compress(zc_ctx* ctx, const void* d_payload, const uint64_t* pay_off, const uint64_t* pay_size,
+                    size_t n, void* d_out, const uint64_t* out_off, uint64_t* out_size);
+/* device time of the last zc_lzo_compress's parse kernel (ms) and its 48 KiB blocks */
+int zc_lzo_last_stats(const zc_ctx* ctx, double* parse_ms, uint64_t* blocks);
+
 int zc_abi_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,152 @@
+"""GPU parity of the bundle writer offload (§8(f)-4), through the C ABI:
+zc_lzo_compress's framed lzo1x_1 output is byte-identical to liblzo2 2.10's
+lzo1x_1_compress + zbackup's framing (compression.cc:435-466, 586-606) for
+every payload -- six kinds of content, the block-edge sizes of
+lzo1x_1_compress's 49152-byte split (20/21 bytes, 49152 + 20/21), random sizes
+up to 3 MB, payloads and outputs at unaligned device offsets -- and a chunked
+stream's new chunks, bundled by Writer::add's rule (chunk_storage.cc:31-46) and
+gathered on the device (Bundle::Creator::addChunk, bundle.cc:30-36), give the
+same bundle files' payload bytes as the oracle's records do."""
+import numpy as np
+import pytest
+
+from oracle import lzo_oracle, oracle
+from tests.lzo_inputs import KINDS, payload
+
+pytestmark = pytest.mark.gpu
+
+EDGE_SIZES = [0, 1, 3, 4, 17, 20, 21, 22, 40, 41, 100, 1000, 49151, 49152, 49153, 49172, 49173, 49174, 98304,
+              98324, 98325, 100000, 262144, 2097152]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    if lzo_oracle.lzo_lib() is None:
+        pytest.skip("liblzo2 not in this image")
+    from zbackup_amd import _build
+    _build.build()
+    oracle.build()
+    return torch
+
+
+@pytest.fixture(scope="module")
+def comp(torch_cuda):
+    from zbackup_amd.bundle import BundleCompressor
+    with BundleCompressor() as c:
+        yield c
+
+
+def _compress(torch, comp, payloads, rng):
+    """All payloads in one zc_lzo_compress call, at odd offsets in and out."""
+    from zbackup_amd.bundle import lzo_capacity
+    pay_off, pos = [], 0
+    for p in payloads:
+        pos += int(rng.integers(0, 16))
+        pay_off.append(pos)
+        pos += len(p)
+    host = np.zeros(pos + 1, dtype=np.uint8)
+    for o, p in zip(pay_off, payloads):
+        host[o:o + len(p)] = p
+    out_off, opos = [], 0
+    for p in payloads:
+        opos += int(rng.integers(0, 16))
+        out_off.append(opos)
+        opos += lzo_capacity(len(p))
+    d_in = torch.from_numpy(host).cuda()
+    d_out = torch.full((opos + 1,), 0xEE, dtype=torch.uint8, device="cuda")
+    sizes = comp.compress(d_in.data_ptr(), pay_off, [len(p) for p in payloads], d_out.data_ptr(), out_off)
+    out = d_out.cpu().numpy()
+    return [out[o:o + int(s)].tobytes() for o, s in zip(out_off, sizes)]
+
+
+def _check(payloads, got):
+    for i, (p, g) in enumerate(zip(payloads, got)):
+        want = lzo_oracle.frame(p.tobytes())
+        assert g == want, f"payload {i}: {len(p)} bytes, got {len(g)} framed bytes, want {len(want)}"
+
+
+def test_lzo_edge_sizes_every_kind(torch_cuda, comp):
+    rng = np.random.default_rng(1)
+    payloads = [payload(k, n, 100 + i) for i, (n, k) in enumerate((n, k) for n in EDGE_SIZES for k in KINDS)]
+    _check(payloads, _compress(torch_cuda, comp, payloads, rng))
+
+
+def test_lzo_random_sizes(torch_cuda, comp):
+    rng = np.random.default_rng(2)
+    payloads = [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 3_000_000)), 200 + i) for i in range(48)]
+    got = _compress(torch_cuda, comp, payloads, rng)
+    _check(payloads, got)
+    for p, g in zip(payloads[:12], got):  # and the library decompresses them
+        assert lzo_oracle.unframe(g) == p.tobytes()
+
+
+def test_lzo_repeated_calls_reuse_dictionaries(torch_cuda, comp):
+    # the dictionaries are not cleared between calls (generation tags): a
+    # second call over different bytes must not see the first call's entries
+    rng = np.random.default_rng(3)
+    for rep in range(3):
+        payloads = [payload(k, 150000 + 977 * rep, 300 + 10 * rep + j) for j, k in enumerate(KINDS)]
+        _check(payloads, _compress(torch_cuda, comp, payloads, rng))
+
+
+def test_lzo_256mib_text_bundles(torch_cuda, comp):
+    rng = np.random.default_rng(4)
+    data = payload("text", 256 << 20, 5)
+    n = 0x200000
+    payloads = [data[i:i + n] for i in range(0, len(data), n)]
+    _check(payloads, _compress(torch_cuda, comp, payloads, rng))
+
+
+@pytest.mark.parametrize("spec_kind", ["mixed", "text"])
+def test_bundles_of_a_chunked_stream(torch_cuda, comp, spec_kind):
+    """stream -> records (GPU) -> NEW chunks the index accepts -> Writer::add
+    bundles -> device gather -> lzo1x_1: every bundle equals the oracle's."""
+    from zbackup_amd import ZC_CHUNK_NEW, BackupCreator
+    from zbackup_amd.bundle import lzo_capacity, plan_bundles
+    torch = torch_cuda
+    W = 65536
+    if spec_kind == "mixed":  # text, random, a repeat of both, zeros
+        a, b = payload("text", 9 << 20, 11), payload("random", 7 << 20, 12)
+        data = np.concatenate([a, b, a[3:5 << 20], np.zeros(3 << 20, np.uint8), b[:4 << 20], payload("runs", 5 << 20, 13)])
+    else:
+        data = payload("text", 40 << 20, 14)
+    want_recs = oracle.chunk_array(data, W)
+    d = torch.from_numpy(data).cuda()
+    with BackupCreator(chunk_max_size=W, sha1=True) as bc:
+        bc.chunk_device(d.data_ptr(), len(data))
+        recs = bc.records()
+    assert len(recs) == len(want_recs)
+    for f in ("offset", "size", "kind", "rolling", "sha1"):
+        assert np.array_equal(recs[f], want_recs[f]), f
+    # Writer::add: saved chunks whose id the index does not hold yet
+    seen, offs, sizes = set(), [], []
+    for r in recs:
+        if r["kind"] != ZC_CHUNK_NEW:
+            continue
+        cid = bytes(r["sha1"]) + int(r["rolling"]).to_bytes(8, "little")
+        if cid in seen:
+            continue
+        seen.add(cid)
+        offs.append(int(r["offset"]))
+        sizes.append(int(r["size"]))
+    bundle_of, nb = plan_bundles(sizes)
+    saved = [r for r in want_recs if r["kind"] == ZC_CHUNK_NEW]
+    want_b = lzo_oracle.writer_bundles(
+        [(bytes(r["sha1"]) + int(r["rolling"]).to_bytes(8, "little"), int(r["size"])) for r in saved])
+    assert nb == len(want_b) and nb > 4
+    d_payload = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device="cuda")
+    comp.gather(d.data_ptr(), offs, sizes, d_payload.data_ptr())
+    pay_size = np.bincount(bundle_of, weights=sizes, minlength=nb).astype(np.uint64)
+    pay_off = np.concatenate([[0], np.cumsum(pay_size)[:-1]]).astype(np.uint64)
+    out_off = np.concatenate([[0], np.cumsum([lzo_capacity(int(s)) for s in pay_size])]).astype(np.uint64)
+    d_out = torch.empty(int(out_off[-1]), dtype=torch.uint8, device="cuda")
+    out_size = comp.compress(d_payload.data_ptr(), pay_off, pay_size, d_out.data_ptr(), out_off[:-1])
+    out = d_out.cpu().numpy()
+    for b, members in enumerate(want_b):
+        pl = b"".join(data[int(saved[m]["offset"]):int(saved[m]["offset"]) + int(saved[m]["size"])].tobytes()
+                      for m in members)
+        got = out[int(out_off[b]):int(out_off[b]) + int(out_size[b])].tobytes()
+        assert got == lzo_oracle.frame(pl), f"bundle {b}"

@@ -8,10 +8,11 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libzchunk.so")
 SOURCES = [os.path.join(CSRC, "zc_kernels.hip"), os.path.join(CSRC, "zc_engine.cpp"),
-           os.path.join(CSRC, "zc_sha256.cpp")]
+           os.path.join(CSRC, "zc_sha256.cpp"), os.path.join(CSRC, "zc_lzo.hip")]
 # host-only sources (no device code; built by the host compiler with x86 intrinsics)
 HOST_ONLY = {"zc_sha256.cpp"}
-HEADERS = [os.path.join(CSRC, "zc_device.h"), os.path.join(ROOT, "include", "zchunk.h")]
+HEADERS = [os.path.join(CSRC, "zc_device.h"), os.path.join(CSRC, "zc_lzo_core.h"),
+           os.path.join(ROOT, "include", "zchunk.h")]
 ARCH = os.environ.get("ZC_OFFLOAD_ARCH", "gfx950")
 
 
@@ -32,7 +33,7 @@ def stale():
 def build(force=False, verbose=False):
     if not force and not stale():
         return LIB
-    objs = []
+    objs, procs = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, os.path.basename(src) + ".o")
         cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
@@ -44,8 +45,11 @@ def build(force=False, verbose=False):
             cmd[1:1] = ["-x", "hip"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), cmd))  # the sources compile in parallel
         objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
     subprocess.run(cmd, check=True)
     for o in objs:

@@ -18,7 +18,8 @@ EXPORTS = ["zc_create", "zc_destroy", "zc_seed_index", "zc_get_input_buffer",
            "zc_get_input_buffer_size", "zc_handle_more_data", "zc_feed", "zc_finish",
            "zc_chunk_device", "zc_record_count", "zc_get_records", "zc_get_stats", "zc_reset",
            "zc_last_error", "zc_fill_splitmix64", "zc_abi_version", "zc_read_stream", "zc_chunk_host",
-           "zc_forget_stream_chunks", "zc_set_window", "zc_get_window", "zc_take_records", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl"]
+           "zc_forget_stream_chunks", "zc_set_window", "zc_get_window", "zc_take_records", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl",
+           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_last_stats"]
 
 
 class ZcRecord(ctypes.Structure):
@@ -87,6 +88,12 @@ def load(path=LIB_PATH):
         "zc_sha256_finish": (i32, [vp, ctypes.c_char_p]),
         "zc_sha256_destroy": (i32, [vp]),
         "zc_sha256_impl": (i32, [vp]),
+        # bundle writer offload (host arrays as pointers: numpy .ctypes.data)
+        "zc_bundle_plan": (i32, [vp, sz, u64, vp, ctypes.POINTER(sz)]),
+        "zc_bundle_gather": (i32, [vp, vp, vp, vp, sz, vp]),
+        "zc_lzo_capacity": (u64, [u64]),
+        "zc_lzo_compress": (i32, [vp, vp, vp, vp, sz, vp, vp, vp]),
+        "zc_lzo_last_stats": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -320,4 +320,21 @@ hipError_t launch_fill_splitmix64(uint8_t* data, uint64_t n, uint64_t seed, hipS
 // Host-side helpers shared with the engine
 uint64_t pow257(uint64_t e);
 
+// zc_lzo.hip: bundle payload assembly + lzo1x_1 compression (zc_lzo_core.h)
+struct LzoScratch;
+struct LzoTimes {
+  double parse_ms;  // zc_lzo_parse_kernel, summed over the call's batches
+  uint64_t blocks;
+};
+LzoScratch* lzo_scratch_new();
+void lzo_scratch_free(LzoScratch* s);
+const LzoTimes* lzo_times(const LzoScratch* s);
+// d_dst <- d_src[off[i] ..+ size[i]) for i = 0 .. n-1, back to back
+hipError_t lzo_gather(LzoScratch* s, const uint8_t* d_src, const uint64_t* off, const uint64_t* size, size_t n,
+                      uint8_t* d_dst, hipStream_t st);
+// payload i = d_payload[pay_off[i] ..+ pay_size[i]) -> framed lzo1x_1 output at
+// d_out + out_off[i]; out_size (host) receives the framed sizes
+hipError_t lzo_compress(LzoScratch* s, const uint8_t* d_payload, const uint64_t* pay_off, const uint64_t* pay_size,
+                        size_t n, uint8_t* d_out, const uint64_t* out_off, uint64_t* out_size, hipStream_t st);
+
 }  // namespace zc

@@ -364,6 +364,8 @@ struct zc_ctx {
   size_t nrec_done = 0;
   zc_stats stats{};
 
+  LzoScratch* lzo = nullptr;  // bundle compression (zc_lzo.hip), made on first use
+
   // scratch
   DevBuf<uint64_t> hm_key, hm_fp;  // metadata of chunks joining the historic index
   DevBuf<uint32_t> hm_anc, hm_g;
@@ -2321,6 +2323,7 @@ int zc_destroy(zc_ctx* c) {
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    lzo_scratch_free(c->lzo);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -2584,3 +2587,86 @@ int zc_fill_splitmix64(void* d_data, uint64_t n, uint64_t seed, int device) {
 }
 
 }  // extern "C"
+
+// ---- bundle writer offload (zc_lzo.hip) ----
+
+int zc_bundle_plan(const uint64_t* sizes, size_t n, uint64_t max_payload, uint32_t* bundle_of, size_t* n_bundles) {
+  if ((n && (!sizes || !bundle_of)) || !n_bundles) return ZC_ERR_ARG;
+  // Writer::add: getCurrentBundle() makes a bundle before the size test, so a
+  // chunk larger than max_payload finishes even an empty current bundle
+  size_t nb = 0;
+  uint64_t payload = 0;
+  bool open = false;
+  for (size_t i = 0; i < n; i++) {
+    if (!open) {
+      open = true;
+      payload = 0;
+      nb++;
+    }
+    if (payload + sizes[i] > max_payload) {
+      nb++;
+      payload = 0;
+    }
+    bundle_of[i] = (uint32_t)(nb - 1);
+    payload += sizes[i];
+  }
+  *n_bundles = nb;
+  return ZC_OK;
+}
+
+static int lzo_fail(zc_ctx* c, hipError_t e, const char* what) {
+  c->err = std::string(what) + ": " + hipGetErrorString(e);
+  return e == hipErrorOutOfMemory ? ZC_ERR_NOMEM : ZC_ERR_HIP;
+}
+
+int zc_bundle_gather(zc_ctx* c, const void* d_src, const uint64_t* src_off, const uint64_t* sizes, size_t n,
+                     void* d_payload) {
+  if (!c || (n && (!d_src || !src_off || !sizes || !d_payload))) return ZC_ERR_ARG;
+  if (!n) return ZC_OK;
+  DeviceGuard g(c->device);
+  if (!c->lzo) c->lzo = lzo_scratch_new();
+  hipError_t e = hipEventRecord(c->ev_in, nullptr);  // after the caller's default-stream work
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+  if (e == hipSuccess)
+    e = lzo_gather(c->lzo, (const uint8_t*)d_src, src_off, sizes, n, (uint8_t*)d_payload, c->stream);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);
+    return lzo_fail(c, e, "zc_bundle_gather");
+  }
+  c->err.clear();
+  return ZC_OK;
+}
+
+uint64_t zc_lzo_capacity(uint64_t payload_size) { return payload_size + payload_size / 16 + 64 + 3 + 16; }
+
+int zc_lzo_compress(zc_ctx* c, const void* d_payload, const uint64_t* pay_off, const uint64_t* pay_size, size_t n,
+                    void* d_out, const uint64_t* out_off, uint64_t* out_size) {
+  if (!c || (n && (!d_payload || !pay_off || !pay_size || !d_out || !out_off || !out_size))) return ZC_ERR_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (pay_size[i] > 0xffffffffull) {  // compression.cc:437-438
+      c->err = "zc_lzo_compress: a payload of 4 GiB or more";
+      return ZC_ERR_ARG;
+    }
+  if (!n) return ZC_OK;
+  DeviceGuard g(c->device);
+  if (!c->lzo) c->lzo = lzo_scratch_new();
+  hipError_t e = hipEventRecord(c->ev_in, nullptr);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+  if (e == hipSuccess)
+    e = lzo_compress(c->lzo, (const uint8_t*)d_payload, pay_off, pay_size, n, (uint8_t*)d_out, out_off, out_size,
+                     c->stream);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);
+    return lzo_fail(c, e, "zc_lzo_compress");
+  }
+  c->err.clear();
+  return ZC_OK;
+}
+
+int zc_lzo_last_stats(const zc_ctx* c, double* parse_ms, uint64_t* blocks) {
+  if (!c) return ZC_ERR_ARG;
+  const LzoTimes t = c->lzo ? *lzo_times(c->lzo) : LzoTimes{};
+  if (parse_ms) *parse_ms = t.parse_ms;
+  if (blocks) *blocks = t.blocks;
+  return ZC_OK;
+}

@@ -1,0 +1,294 @@
+// zc_lzo.hip -- bundle writer offload: Bundle::Creator::addChunk's payload
+// assembly (bundle.cc:30-36) and the lzo1x_1 compression of
+// Bundle::Creator::write (bundle.cc:120-151 -> LZO1X_1_Encoder::doProcessNoSize,
+// compression.cc:586-606, i.e. liblzo2 2.10's lzo1x_1_compress) with zbackup's
+// framing, on the GPU, byte-identical to the library's output.
+//
+// Work split (zc_lzo_core.h explains why the blocks are independent):
+//   zc_lzo_parse_kernel  one lane per 48 KiB block: the greedy parse over a
+//                        2^14-entry dictionary of its own (u32 entries tagged
+//                        with the call's generation in HBM, so no per-block
+//                        memset), staging the block's encoding from its first
+//                        match on;
+//   zc_lzo_chain_kernel  one lane per bundle: walks its blocks in order, writes
+//                        the frame, first-literal-run headers, final run and
+//                        end marker, and lists the byte copies;
+//   zc_lzo_copy_kernel   one wave per copy (literal runs from the payload,
+//                        staged encodings), 16-byte stores aligned on the
+//                        destination;
+//   zc_lzo_or_kernel     a final run of 1-3 literals or-ed into the last match.
+// The same copy kernel gathers chunk extents into bundle payloads.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#define ZC_HD __host__ __device__
+#include "zc_device.h"
+#include "zc_lzo_core.h"
+
+namespace zc {
+
+using zclzo::BlkOut;
+using zclzo::kDictSize;
+using zclzo::kStageCap;
+
+namespace {
+
+struct BlkDesc {
+  uint64_t start;  // offset in the payload buffer
+  uint32_t ll;
+  uint32_t first;  // a payload's first block (inherits no literals)
+};
+struct BundleDesc {
+  uint64_t pay_off, pay_size, out_off;
+  uint32_t blk0, copy0;
+};
+struct Copy {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint64_t n;
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct TagDict {
+  uint32_t* d;
+  uint32_t tag;  // generation << 16
+  __device__ uint32_t exchange(uint32_t i, uint32_t pos) {
+    const uint32_t o = d[i];
+    d[i] = tag | pos;
+    return (o & 0xffff0000u) == tag ? (o & 0xffffu) : 0u;
+  }
+};
+
+__global__ __launch_bounds__(64) void zc_lzo_parse_kernel(const uint8_t* __restrict__ payload,
+                                                          const BlkDesc* __restrict__ blks, uint32_t nblk,
+                                                          uint32_t* __restrict__ dict, uint32_t tag,
+                                                          uint8_t* __restrict__ stage, BlkOut* __restrict__ out) {
+  const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= nblk) return;
+  const BlkDesc d = blks[b];
+  TagDict td{dict + (size_t)b * kDictSize, tag << 16};
+  out[b] = zclzo::parse_block(payload + d.start, d.ll, d.first ? 0u : 4u, td, stage + (size_t)b * kStageCap);
+}
+
+__global__ __launch_bounds__(64) void zc_lzo_chain_kernel(const uint8_t* __restrict__ payload,
+                                                          const BundleDesc* __restrict__ bund, uint32_t nb,
+                                                          const BlkOut* __restrict__ bo,
+                                                          const uint8_t* __restrict__ stage, uint8_t* __restrict__ out,
+                                                          Copy* __restrict__ copies, uint64_t* __restrict__ out_size,
+                                                          uint64_t* __restrict__ or_at, uint32_t* __restrict__ or_val) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nb) return;
+  const BundleDesc d = bund[i];
+  uint8_t* o = out + d.out_off;
+  Copy* c = copies + d.copy0;
+  uint32_t nc = 0;
+  auto copy = [&](bool from_stage, uint64_t src, uint64_t dst, uint64_t n) {
+    if (!n) return;
+    c[nc++] = Copy{from_stage ? stage + (size_t)(d.blk0 + src) * kStageCap : payload + d.pay_off + src, o + dst, n};
+  };
+  uint64_t oa;
+  uint32_t ov;
+  out_size[i] = zclzo::chain_bundle(d.pay_size, bo + d.blk0, o, copy, &oa, &ov);
+  const uint32_t cap = zclzo::copies_cap(zclzo::block_count(d.pay_size));
+  for (uint32_t k = nc; k < cap; k++) c[k].n = 0;
+  or_at[i] = d.out_off + oa;
+  or_val[i] = ov;
+}
+
+// one wave per copy: a head of bytes up to the destination's 16-byte
+// alignment, 16-byte aligned stores (the source read unaligned), a byte tail
+__global__ __launch_bounds__(256) void zc_lzo_copy_kernel(const Copy* __restrict__ copies, uint32_t n) {
+  const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (w >= n) return;
+  const Copy c = copies[w];
+  if (!c.n) return;
+  uint64_t len = c.n;
+  const uint8_t* src = c.src;
+  uint8_t* dst = c.dst;
+  uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+  if (head > len) head = (uint32_t)len;
+  if (lane < head) dst[lane] = src[lane];
+  src += head;
+  dst += head;
+  len -= head;
+  const uint64_t nv = len >> 4;
+  for (uint64_t v = lane; v < nv; v += 64) {
+    u32x4 x;
+    __builtin_memcpy(&x, src + v * 16, 16);
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst + v * 16));
+  }
+  const uint32_t t = (uint32_t)(len & 15);
+  if (lane < t) dst[nv * 16 + lane] = src[nv * 16 + lane];
+}
+
+__global__ void zc_lzo_or_kernel(uint8_t* out, const uint64_t* or_at, const uint32_t* or_val, uint32_t nb) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb && or_val[i]) out[or_at[i]] |= (uint8_t)or_val[i];
+}
+
+template <class T>
+struct Buf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n, bool zero = false) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = n;
+    if (zero) e = hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(T));
+    return e;
+  }
+  ~Buf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+#define LCK(x)                            \
+  do {                                    \
+    hipError_t e_ = (x);                  \
+    if (e_ != hipSuccess) return e_;      \
+  } while (0)
+
+// at most this many blocks per device batch (12 GiB of payload; the
+// dictionaries take 64 KiB and the staging 51 KiB per block)
+constexpr uint32_t kMaxBatchBlocks = 1u << 18;
+
+}  // namespace
+
+struct LzoScratch {
+  Buf<uint32_t> dict;
+  Buf<uint8_t> stage;
+  Buf<BlkOut> bo;
+  Buf<BlkDesc> blks;
+  Buf<BundleDesc> bund;
+  Buf<Copy> copies;
+  Buf<uint64_t> out_size, or_at;
+  Buf<uint32_t> or_val;
+  uint32_t gen = 0;  // tag of the dictionaries' live entries
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  LzoTimes times{};
+};
+
+LzoScratch* lzo_scratch_new() { return new LzoScratch(); }
+void lzo_scratch_free(LzoScratch* s) {
+  if (!s) return;
+  if (s->e0) (void)hipEventDestroy(s->e0);
+  if (s->e1) (void)hipEventDestroy(s->e1);
+  delete s;
+}
+const LzoTimes* lzo_times(const LzoScratch* s) { return &s->times; }
+
+hipError_t lzo_copy_list(LzoScratch* s, const std::vector<Copy>& list, hipStream_t st) {
+  if (list.empty()) return hipSuccess;
+  LCK(s->copies.ensure(list.size()));
+  LCK(hipMemcpyAsync(s->copies.p, list.data(), list.size() * sizeof(Copy), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(zc_lzo_copy_kernel, dim3((uint32_t)((list.size() + 3) / 4)), dim3(256), 0, st, s->copies.p,
+                     (uint32_t)list.size());
+  LCK(hipGetLastError());
+  return hipStreamSynchronize(st);  // the list's host memory is reused
+}
+
+hipError_t lzo_gather(LzoScratch* s, const uint8_t* d_src, const uint64_t* off, const uint64_t* size, size_t n,
+                      uint8_t* d_dst, hipStream_t st) {
+  // pieces of at most 1 MiB, so one long extent is not one wave's work
+  constexpr uint64_t kPiece = 1ull << 20;
+  std::vector<Copy> list;
+  uint64_t pos = 0;
+  for (size_t i = 0; i < n; i++) {
+    for (uint64_t k = 0; k < size[i]; k += kPiece)
+      list.push_back(Copy{d_src + off[i] + k, d_dst + pos + k, std::min(kPiece, size[i] - k)});
+    pos += size[i];
+  }
+  return lzo_copy_list(s, list, st);
+}
+
+static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint64_t* pay_off,
+                            const uint64_t* pay_size, size_t b0, size_t b1, uint8_t* d_out, const uint64_t* out_off,
+                            uint64_t* out_size, hipStream_t st) {
+  std::vector<BlkDesc> blks;
+  std::vector<BundleDesc> bund;
+  uint32_t ncopy = 0;
+  for (size_t i = b0; i < b1; i++) {
+    const uint32_t nblk = zclzo::block_count(pay_size[i]);
+    bund.push_back(BundleDesc{pay_off[i], pay_size[i], out_off[i], (uint32_t)blks.size(), ncopy});
+    uint64_t pos = 0;
+    for (uint32_t k = 0; k < nblk; k++) {
+      const uint32_t ll = (uint32_t)std::min<uint64_t>(pay_size[i] - pos, zclzo::kBlock);
+      blks.push_back(BlkDesc{pay_off[i] + pos, ll, k == 0 ? 1u : 0u});
+      pos += ll;
+    }
+    ncopy += zclzo::copies_cap(nblk);
+  }
+  const uint32_t nblk = (uint32_t)blks.size(), nb = (uint32_t)bund.size();
+  // dictionaries: entries of an earlier generation read as empty; zeroed
+  // when (re)allocated and when the 16-bit generation wraps
+  if (s->dict.cap < (size_t)nblk * kDictSize) {
+    LCK(s->dict.ensure((size_t)nblk * kDictSize, true));
+    s->gen = 0;
+  } else if (s->gen == 0xffff) {
+    LCK(hipMemsetAsync(s->dict.p, 0, s->dict.cap * sizeof(uint32_t), st));
+    s->gen = 0;
+  }
+  const uint32_t tag = ++s->gen;
+  LCK(s->stage.ensure((size_t)nblk * kStageCap));
+  LCK(s->bo.ensure(nblk));
+  LCK(s->blks.ensure(nblk));
+  LCK(s->bund.ensure(nb));
+  LCK(s->copies.ensure(ncopy));
+  LCK(s->out_size.ensure(nb));
+  LCK(s->or_at.ensure(nb));
+  LCK(s->or_val.ensure(nb));
+  if (!s->e0) LCK(hipEventCreate(&s->e0));
+  if (!s->e1) LCK(hipEventCreate(&s->e1));
+  if (nblk) LCK(hipMemcpyAsync(s->blks.p, blks.data(), nblk * sizeof(BlkDesc), hipMemcpyHostToDevice, st));
+  LCK(hipMemcpyAsync(s->bund.p, bund.data(), nb * sizeof(BundleDesc), hipMemcpyHostToDevice, st));
+  LCK(hipEventRecord(s->e0, st));
+  if (nblk)
+    hipLaunchKernelGGL(zc_lzo_parse_kernel, dim3((nblk + 63) / 64), dim3(64), 0, st, d_payload, s->blks.p, nblk,
+                       s->dict.p, tag, s->stage.p, s->bo.p);
+  LCK(hipEventRecord(s->e1, st));
+  hipLaunchKernelGGL(zc_lzo_chain_kernel, dim3((nb + 63) / 64), dim3(64), 0, st, d_payload, s->bund.p, nb, s->bo.p,
+                     s->stage.p, d_out, s->copies.p, s->out_size.p, s->or_at.p, s->or_val.p);
+  if (ncopy)
+    hipLaunchKernelGGL(zc_lzo_copy_kernel, dim3((ncopy + 3) / 4), dim3(256), 0, st, s->copies.p, ncopy);
+  hipLaunchKernelGGL(zc_lzo_or_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, d_out, s->or_at.p, s->or_val.p, nb);
+  LCK(hipGetLastError());
+  LCK(hipMemcpyAsync(out_size + b0, s->out_size.p, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  LCK(hipStreamSynchronize(st));
+  float ms = 0;
+  LCK(hipEventElapsedTime(&ms, s->e0, s->e1));
+  s->times.parse_ms += ms;
+  s->times.blocks += nblk;
+  return hipSuccess;
+}
+
+hipError_t lzo_compress(LzoScratch* s, const uint8_t* d_payload, const uint64_t* pay_off, const uint64_t* pay_size,
+                        size_t n, uint8_t* d_out, const uint64_t* out_off, uint64_t* out_size, hipStream_t st) {
+  s->times = LzoTimes{};
+  size_t b0 = 0;
+  while (b0 < n) {
+    size_t b1 = b0;
+    uint64_t blk = 0;
+    while (b1 < n) {
+      const uint32_t k = zclzo::block_count(pay_size[b1]);
+      if (b1 > b0 && blk + k > kMaxBatchBlocks) break;
+      blk += k;
+      b1++;
+    }
+    LCK(lzo_batch(s, d_payload, pay_off, pay_size, b0, b1, d_out, out_off, out_size, st));
+    b0 = b1;
+  }
+  return hipSuccess;
+}
+
+}  // namespace zc
