@@ -22,6 +22,9 @@ names), the same line carries, driver-observed:
                hash on every record: backup_creator.cc:130-131, chunk_id.cc:19-27)
   end_to_end   the stream starting in pinned host memory (zc_chunk_host: H2D
                overlapped with the scan), the zutils.cc:100-124 path
+  bundle_lzo   the bundle writer offload: saved chunks bundled (Writer::add),
+               gathered and lzo1x_1-compressed on the GPU (bundle.cc:30-36,
+               96-155), with liblzo2 on one core beside it
 """
 import argparse
 import json
@@ -56,6 +59,8 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-sample-mib", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lzo", dest="lzo", action="store_false",
+                    help="skip the bundle_lzo (bundle writer offload) pass")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only (skip the value_sha1 and end_to_end passes)")
     ap.add_argument("--sha1-steps", type=int, default=5)
@@ -244,6 +249,64 @@ def timed_steps(torch, world, step, warmup, steps):
     return job_elapsed(time.perf_counter() - t0, world), scan
 
 
+def bundle_leg(torch, buf, n, recs, world, local, cpu_sample):
+    """Bundle writer offload (§8(f)-4) over the stream's saved chunks: Writer::add's
+    bundling (2 MiB bundles), the payloads gathered on the device and lzo1x_1
+    compressed with zbackup's framing -- for the C2 stream (random: LZO finds
+    nothing to match) and for 4 GiB of text-like data (compresses ~3x); liblzo2
+    on one core over 64 MiB of each as the CPU baseline."""
+    import numpy as np
+
+    from tests.lzo_inputs import payload
+    from zbackup_amd import ZC_CHUNK_NEW
+    from zbackup_amd.bundle import BundleCompressor, lzo_capacity, plan_bundles
+    res = {}
+    with BundleCompressor(device=local) as comp:
+        for kind in ("random", "text"):
+            if kind == "random":
+                src, nbytes = buf, n
+                sel = recs[recs["kind"] == ZC_CHUNK_NEW]
+                offs, sizes = sel["offset"].astype(np.uint64), sel["size"].astype(np.uint64)
+            else:
+                nbytes = 4 << 30
+                base = payload("text", 128 << 20, 21)
+                src = torch.from_numpy(np.resize(base, nbytes)).to(buf.device)
+                offs = np.arange(0, nbytes, W64, dtype=np.uint64)
+                sizes = np.full(len(offs), W64, dtype=np.uint64)
+            bundle_of, nb = plan_bundles(sizes)
+            pay_size = np.bincount(bundle_of, weights=sizes, minlength=nb).astype(np.uint64)
+            pay_off = np.concatenate([[0], np.cumsum(pay_size)[:-1]]).astype(np.uint64)
+            caps = np.array([lzo_capacity(int(x)) for x in pay_size], dtype=np.uint64)
+            out_off = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.uint64)
+            d_pay = torch.empty(int(pay_size.sum()), dtype=torch.uint8, device=buf.device)
+            d_out = torch.empty(int(caps.sum()), dtype=torch.uint8, device=buf.device)
+
+            def step():
+                comp.gather(src.data_ptr(), offs, sizes, d_pay.data_ptr())
+                step.sizes = comp.compress(d_pay.data_ptr(), pay_off, pay_size, d_out.data_ptr(), out_off)
+                return 0.0
+
+            el, _ = timed_steps(torch, world, step, 1, 3)
+            parse_ms, blocks = comp.last_stats()
+            in_bytes = int(sizes.sum())
+            r = {"value": round(job_value(in_bytes, world, 3, el), 3), "unit": "GiB/s",
+                 "ms_per_step": round(el / 3 * 1e3, 3), "bundles": int(nb), "blocks_48k": int(blocks),
+                 "parse_ms": round(parse_ms, 3), "ratio": round(float(step.sizes.sum()) / in_bytes, 4)}
+            if cpu_sample:
+                from oracle import lzo_oracle
+                if lzo_oracle.lzo_lib() is not None:
+                    host = d_pay[:64 << 20].cpu().numpy()
+                    t0 = time.perf_counter()
+                    for i in range(0, len(host), 0x200000):
+                        lzo_oracle.frame(host[i:i + 0x200000].tobytes())
+                    r["cpu_liblzo2_1core"] = round(len(host) / (time.perf_counter() - t0) / 2**30, 4)
+            res[kind] = r
+            del d_pay, d_out, src
+    res["path"] = ("saved chunks -> Writer::add bundles (2 MiB) -> zc_bundle_gather (HBM) -> zc_lzo_compress "
+                   "(lzo1x_1 + zbackup framing, byte-identical to liblzo2 2.10)")
+    return res
+
+
 def rank_env(args):
     """(world, rank, local rank) from the environment; joins the gloo group
     the replicas use for their barriers and max/gather reductions."""
@@ -327,7 +390,8 @@ def run_rank(args):
     bc = BackupCreator(W64, device=local, sha1=args.sha1, timing=True)
     elapsed, scan_ms = timed_steps(torch, world, make_step(bc, args.sha1), args.warmup, args.steps)
     st = bc.stats()
-    nrec = len(bc.records())
+    recs = bc.records().copy()
+    nrec = len(recs)
     bc.close()
     ms_step = elapsed / args.steps * 1e3
     value = job_value(n, world, args.steps, elapsed)
@@ -427,6 +491,8 @@ def run_rank(args):
                           "records": nrec_feed, "segments": fst["segments"], "hbm_bytes": fst["hbm_bytes"],
                           "host_memcpy_s": round(copy_s, 4), "feed_s": round(feed_s, 4)}
         del host
+        if args.config == "c2" and args.lzo:
+            extras["bundle_lzo"] = bundle_leg(torch, buf, n, recs, world, local, rank == 0)
 
     cpu = None
     if not args.no_cpu_baseline and args.config == "c2":
@@ -496,6 +562,8 @@ def run_rank(args):
             f = extras["feed"]
             f["value"] = round(f["value"], 3)
             out["feed"] = f
+        if "bundle_lzo" in extras:
+            out["bundle_lzo"] = extras["bundle_lzo"]
         if cpu:
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

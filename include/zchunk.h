@@ -200,6 +200,11 @@ int zc_bundle_gather(zc_ctx* ctx, const void* d_src, const uint64_t* src_off, co
 uint64_t zc_lzo_capacity(uint64_t payload_size); /* LZO1X_1_Encoder::suggestOutputSize + 16 */
 int zc_lzo_compress(zc_ctx* ctx, const void* d_payload, const uint64_t* pay_off, const uint64_t* pay_size,
                     size_t n, void* d_out, const uint64_t* out_off, uint64_t* out_size);
+/* the same for payloads in host memory (copied to HBM, compressed, copied back to
+ * out + out_off[i]): the form Bundle::Creator::write can call per finished bundle (or per
+ * batch of them) without device buffers of its own */
+int zc_lzo_compress_host(zc_ctx* ctx, const void* payload, const uint64_t* pay_off, const uint64_t* pay_size,
+                         size_t n, void* out, const uint64_t* out_off, uint64_t* out_size);
 /* device time of the last zc_lzo_compress's parse kernel (ms) and its 48 KiB blocks */
 int zc_lzo_last_stats(const zc_ctx* ctx, double* parse_ms, uint64_t* blocks);
 

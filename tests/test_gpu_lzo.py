@@ -92,6 +92,11 @@ def test_lzo_repeated_calls_reuse_dictionaries(torch_cuda, comp):
         _check(payloads, _compress(torch_cuda, comp, payloads, rng))
 
 
+def test_lzo_compress_host(torch_cuda, comp):
+    payloads = [payload(k, 70000 + 4099 * i, 400 + i) for i, k in enumerate(KINDS)] + [np.zeros(0, np.uint8)]
+    _check(payloads, comp.compress_host([p.tobytes() for p in payloads]))
+
+
 def test_lzo_256mib_text_bundles(torch_cuda, comp):
     rng = np.random.default_rng(4)
     data = payload("text", 256 << 20, 5)

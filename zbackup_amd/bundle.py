@@ -71,6 +71,21 @@ class BundleCompressor:
         _check(self._L, self._ctx, rc, "zc_lzo_compress")
         return out_size
 
+    def compress_host(self, payloads):
+        """Host bytes in, framed bytes out (zc_lzo_compress_host), one call for all."""
+        payloads = [bytes(p) for p in payloads]
+        sizes = np.array([len(p) for p in payloads], dtype=np.uint64)
+        pay_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64) if len(sizes) else sizes
+        caps = np.array([lzo_capacity(int(s)) for s in sizes], dtype=np.uint64)
+        out_off = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.uint64) if len(caps) else caps
+        src = np.frombuffer(b"".join(payloads) or b"\0", dtype=np.uint8)
+        out = np.zeros(int(caps.sum()) or 1, dtype=np.uint8)
+        out_size = np.zeros(len(sizes), dtype=np.uint64)
+        rc = self._L.zc_lzo_compress_host(self._ctx, src.ctypes.data, pay_off.ctypes.data, sizes.ctypes.data,
+                                          len(sizes), out.ctypes.data, out_off.ctypes.data, out_size.ctypes.data)
+        _check(self._L, self._ctx, rc, "zc_lzo_compress_host")
+        return [out[int(o):int(o) + int(s)].tobytes() for o, s in zip(out_off, out_size)]
+
     def last_stats(self):
         """(parse kernel ms, 48 KiB blocks) of the last compress()."""
         ms, blocks = ctypes.c_double(), ctypes.c_uint64()

@@ -365,6 +365,7 @@ struct zc_ctx {
   zc_stats stats{};
 
   LzoScratch* lzo = nullptr;  // bundle compression (zc_lzo.hip), made on first use
+  DevBuf<uint8_t> lzo_in, lzo_out;  // zc_lzo_compress_host's device copies
 
   // scratch
   DevBuf<uint64_t> hm_key, hm_fp;  // metadata of chunks joining the historic index
@@ -2661,6 +2662,33 @@ int zc_lzo_compress(zc_ctx* c, const void* d_payload, const uint64_t* pay_off, c
   }
   c->err.clear();
   return ZC_OK;
+}
+
+int zc_lzo_compress_host(zc_ctx* c, const void* payload, const uint64_t* pay_off, const uint64_t* pay_size,
+                         size_t n, void* out, const uint64_t* out_off, uint64_t* out_size) {
+  if (!c || (n && (!payload || !pay_off || !pay_size || !out || !out_off || !out_size))) return ZC_ERR_ARG;
+  uint64_t in_end = 0, out_end = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (pay_size[i] > 0xffffffffull) {
+      c->err = "zc_lzo_compress_host: a payload of 4 GiB or more";
+      return ZC_ERR_ARG;
+    }
+    in_end = std::max(in_end, pay_off[i] + pay_size[i]);
+    out_end = std::max(out_end, out_off[i] + zc_lzo_capacity(pay_size[i]));
+  }
+  if (!n) return ZC_OK;
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    if (!c->lzo) c->lzo = lzo_scratch_new();
+    c->lzo_in.ensure(in_end);
+    c->lzo_out.ensure(out_end);
+    HCK(hipMemcpyAsync(c->lzo_in.p, payload, in_end, hipMemcpyHostToDevice, c->stream));
+    HCK(lzo_compress(c->lzo, c->lzo_in.p, pay_off, pay_size, n, c->lzo_out.p, out_off, out_size, c->stream));
+    for (size_t i = 0; i < n; i++)
+      HCK(hipMemcpyAsync((uint8_t*)out + out_off[i], c->lzo_out.p + out_off[i], out_size[i], hipMemcpyDeviceToHost,
+                         c->stream));
+    HCK(hipStreamSynchronize(c->stream));
+  });
 }
 
 int zc_lzo_last_stats(const zc_ctx* c, double* parse_ms, uint64_t* blocks) {

@@ -42,7 +42,8 @@ struct BlkDesc {
 };
 struct BundleDesc {
   uint64_t pay_off, pay_size, out_off;
-  uint32_t blk0, copy0;
+  uint32_t blk0;
+  uint64_t copy0;
 };
 struct Copy {
   const uint8_t* src;
@@ -84,16 +85,18 @@ __global__ __launch_bounds__(64) void zc_lzo_chain_kernel(const uint8_t* __restr
   const BundleDesc d = bund[i];
   uint8_t* o = out + d.out_off;
   Copy* c = copies + d.copy0;
-  uint32_t nc = 0;
+  uint64_t nc = 0;
+  // pieces of at most 64 KiB, one wave's work each
   auto copy = [&](bool from_stage, uint64_t src, uint64_t dst, uint64_t n) {
-    if (!n) return;
-    c[nc++] = Copy{from_stage ? stage + (size_t)(d.blk0 + src) * kStageCap : payload + d.pay_off + src, o + dst, n};
+    const uint8_t* s = from_stage ? stage + (size_t)(d.blk0 + src) * kStageCap : payload + d.pay_off + src;
+    for (uint64_t k = 0; k < n; k += zclzo::kPiece)
+      c[nc++] = Copy{s + k, o + dst + k, n - k < zclzo::kPiece ? n - k : zclzo::kPiece};
   };
   uint64_t oa;
   uint32_t ov;
   out_size[i] = zclzo::chain_bundle(d.pay_size, bo + d.blk0, o, copy, &oa, &ov);
-  const uint32_t cap = zclzo::copies_cap(zclzo::block_count(d.pay_size));
-  for (uint32_t k = nc; k < cap; k++) c[k].n = 0;
+  const uint64_t cap = zclzo::copies_cap(zclzo::block_count(d.pay_size), d.pay_size);
+  for (uint64_t k = nc; k < cap; k++) c[k].n = 0;
   or_at[i] = d.out_off + oa;
   or_val[i] = ov;
 }
@@ -200,8 +203,8 @@ hipError_t lzo_copy_list(LzoScratch* s, const std::vector<Copy>& list, hipStream
 
 hipError_t lzo_gather(LzoScratch* s, const uint8_t* d_src, const uint64_t* off, const uint64_t* size, size_t n,
                       uint8_t* d_dst, hipStream_t st) {
-  // pieces of at most 1 MiB, so one long extent is not one wave's work
-  constexpr uint64_t kPiece = 1ull << 20;
+  // pieces of at most 64 KiB, so one long extent is not one wave's work
+  constexpr uint64_t kPiece = zclzo::kPiece;
   std::vector<Copy> list;
   uint64_t pos = 0;
   for (size_t i = 0; i < n; i++) {
@@ -217,7 +220,7 @@ static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint6
                             uint64_t* out_size, hipStream_t st) {
   std::vector<BlkDesc> blks;
   std::vector<BundleDesc> bund;
-  uint32_t ncopy = 0;
+  uint64_t ncopy = 0;
   for (size_t i = b0; i < b1; i++) {
     const uint32_t nblk = zclzo::block_count(pay_size[i]);
     bund.push_back(BundleDesc{pay_off[i], pay_size[i], out_off[i], (uint32_t)blks.size(), ncopy});
@@ -227,7 +230,7 @@ static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint6
       blks.push_back(BlkDesc{pay_off[i] + pos, ll, k == 0 ? 1u : 0u});
       pos += ll;
     }
-    ncopy += zclzo::copies_cap(nblk);
+    ncopy += zclzo::copies_cap(nblk, pay_size[i]);
   }
   const uint32_t nblk = (uint32_t)blks.size(), nb = (uint32_t)bund.size();
   // dictionaries: entries of an earlier generation read as empty; zeroed
@@ -260,7 +263,8 @@ static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint6
   hipLaunchKernelGGL(zc_lzo_chain_kernel, dim3((nb + 63) / 64), dim3(64), 0, st, d_payload, s->bund.p, nb, s->bo.p,
                      s->stage.p, d_out, s->copies.p, s->out_size.p, s->or_at.p, s->or_val.p);
   if (ncopy)
-    hipLaunchKernelGGL(zc_lzo_copy_kernel, dim3((ncopy + 3) / 4), dim3(256), 0, st, s->copies.p, ncopy);
+    hipLaunchKernelGGL(zc_lzo_copy_kernel, dim3((uint32_t)((ncopy + 3) / 4)), dim3(256), 0, st, s->copies.p,
+                       (uint32_t)ncopy);
   hipLaunchKernelGGL(zc_lzo_or_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, d_out, s->or_at.p, s->or_val.p, nb);
   LCK(hipGetLastError());
   LCK(hipMemcpyAsync(out_size + b0, s->out_size.p, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));

@@ -135,13 +135,20 @@ ZC_HD inline BlkOut parse_block(const uint8_t* in, uint32_t ll, uint32_t ti, Dic
   uint32_t ii = 0;
   uint8_t* op = stage;
   BlkOut r{0, 0, 0, 0};
+  ip += 1 + ((ip - ii) >> 5);  // the first probe (the loop's "literal" step)
+  uint32_t dv = ip < ip_end ? ld32(in + ip) : 0;
   for (;;) {
-    ip += 1 + ((ip - ii) >> 5);  // literal
-  next:
     if (ip >= ip_end) break;
-    uint32_t dv = ld32(in + ip);
-    uint32_t m = dict.exchange(dindex(dv), ip);
-    if (dv != ld32(in + m)) continue;
+    const uint32_t m = dict.exchange(dindex(dv), ip);
+    // the next probe of a literal run and its bytes, loaded while the
+    // dictionary entry's bytes are (the step depends on ip and ii only)
+    const uint32_t ip_lit = ip + 1 + ((ip - ii) >> 5);
+    const uint32_t dv_lit = ip_lit < ip_end ? ld32(in + ip_lit) : 0;
+    if (dv != ld32(in + m)) {
+      ip = ip_lit;
+      dv = dv_lit;
+      continue;
+    }
     // a match: extend it 8 bytes at a time, stopping once past ip_end
     uint32_t m_len = 4;
     uint64_t v = ld64(in + ip + m_len) ^ ld64(in + m + m_len);
@@ -174,7 +181,7 @@ ZC_HD inline BlkOut parse_block(const uint8_t* in, uint32_t ll, uint32_t ti, Dic
     }
     ip += m_len;
     ii = ip;
-    goto next;
+    if (ip < ip_end) dv = ld32(in + ip);
   }
   r.tail = ll - ii;
   r.staged = (uint32_t)(op - stage);
@@ -209,8 +216,10 @@ ZC_HD inline uint32_t block_count(uint64_t n) {
 }
 
 // copies chain_bundle asks for (literal runs from the payload, staged
-// encodings); at most 2 per block + 1
-constexpr uint32_t copies_cap(uint32_t nblk) { return 2 * nblk + 1; }
+// encodings): at most 2 per block + 1; split into pieces of at most kPiece
+// bytes, at most one more piece per kPiece of output
+constexpr uint64_t kPiece = 1u << 16;
+ZC_HD inline uint64_t copies_cap(uint32_t nblk, uint64_t n) { return 2ull * nblk + 1 + frame_capacity(n) / kPiece + 1; }
 
 // Assemble one bundle (DO_COMPRESS in lzo1x_c.ch after the block loop, and the
 // framing): writes the frame, every block's first literal-run header, the final
