@@ -179,4 +179,58 @@ public:
   }
 };
 
+/// lzo1x_1 of finished bundles on the GPU, for Bundle::Creator::write
+/// (bundle.cc:96-155) when the selected compression is "lzo1x_1": the framed
+/// bytes equal what LZO1X_1_Encoder writes (compression.cc:435-466, 586-606),
+/// so the encoder loop there becomes
+///
+///   string framed;
+///   gpuLzo.compress( payload, framed );    // one payload, or compressAll for a batch
+///   os.write( framed.data(), framed.size() );
+///
+/// (EncryptedFile::OutputStream::write, as bundle.cc:84 uses it), followed by the
+/// os.writeAdler32() the reference already does.
+class GpuLzoBundleCompressor: NoCopy
+{
+  zc_ctx * ctx;
+
+public:
+  explicit GpuLzoBundleCompressor( GpuChunkIndex & index ): ctx( index.context() ) {}
+
+  void compress( string const & payload, string & framed )
+  {
+    std::vector< string const * > one( 1, &payload );
+    std::vector< string > out;
+    compressAll( one, out );
+    framed.swap( out[ 0 ] );
+  }
+
+  /// several finished bundles in one device call (Writer::finishCurrentBundle
+  /// can queue them instead of starting a compressor thread per bundle)
+  void compressAll( std::vector< string const * > const & payloads, std::vector< string > & framed )
+  {
+    size_t n = payloads.size();
+    std::vector< uint64_t > payOff( n ), paySize( n ), outOff( n ), outSize( n );
+    string in, out;
+    uint64_t inPos = 0, outPos = 0;
+    for ( size_t i = 0; i < n; ++i )
+    {
+      payOff[ i ] = inPos;
+      paySize[ i ] = payloads[ i ]->size();
+      inPos += paySize[ i ];
+      outOff[ i ] = outPos;
+      outPos += zc_lzo_capacity( paySize[ i ] );
+    }
+    in.reserve( inPos );
+    for ( size_t i = 0; i < n; ++i )
+      in += *payloads[ i ];
+    out.resize( outPos ? outPos : 1 );
+    zcCheck( zc_lzo_compress_host( ctx, in.data(), payOff.data(), paySize.data(), n, &out[ 0 ], outOff.data(),
+                                   outSize.data() ), ctx, "zc_lzo_compress_host" );
+    framed.resize( n );
+    for ( size_t i = 0; i < n; ++i )
+      framed[ i ].assign( out, outOff[ i ], outSize[ i ] );
+  }
+};
+
 #endif
