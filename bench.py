@@ -269,8 +269,9 @@ def bundle_leg(torch, buf, n, recs, world, local, cpu_sample):
                 offs, sizes = sel["offset"].astype(np.uint64), sel["size"].astype(np.uint64)
             else:
                 nbytes = 4 << 30
-                base = payload("text", 128 << 20, 21)
-                src = torch.from_numpy(np.resize(base, nbytes)).to(buf.device)
+                base = torch.from_numpy(payload("text", 128 << 20, 21)).to(buf.device)
+                src = base.repeat(nbytes // base.numel())  # built in HBM (no 4 GiB host array per rank)
+                del base
                 offs = np.arange(0, nbytes, W64, dtype=np.uint64)
                 sizes = np.full(len(offs), W64, dtype=np.uint64)
             bundle_of, nb = plan_bundles(sizes)

@@ -3,7 +3,8 @@
 #   bench lines (C2 with the CPU baseline and the value_sha1 / end_to_end / feed
 #   passes, C3, C5, C2 with SHA-1 ids as the headline), rocprofv3
 #   kernel-trace summaries of C2/C3/C5, the scan's FETCH_SIZE and WRITE_SIZE
-#   passes and one SQ-counter pass (separate runs), and the host CPU description.
+#   passes and one SQ-counter pass (separate runs), the bundle compressor's
+#   kernel trace (tools/lzo_rate.py), and the host CPU description.
 #   bash tools/profile_round.sh OUTDIR
 set -e
 OUT=${1:-gpurun_out/prof_round}
@@ -24,5 +25,7 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
   SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o s -- \
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > "$OUT/pmc_sq.log" 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace_lzo" -o lzo -- \
+  python3 tools/lzo_rate.py 4 random text > "$OUT/trace_lzo.log" 2>&1
 (lscpu; echo; echo "nproc: $(nproc)") > "$OUT/host_cpu.txt"
 echo done
