@@ -400,7 +400,10 @@ def run_rank(args):
     fracs = [n / (s * 1e-3) / 1e9 / HBM_PEAK_GBS for s in job_gather(scan_avg, world)]
 
     extras = {}
-    if not args.no_extras:
+    # the extra passes are single-GPU measurements: a multi-GPU run (C4) keeps
+    # to the headline, the per-GPU fractions and the concurrent CPU baseline, so
+    # N ranks do not each pin 8 GiB of host memory for the end-to-end legs
+    if not args.no_extras and world == 1:
         # complete ChunkIds on every record, same streams
         if not args.sha1 and args.sha1_steps > 0:
             b2 = BackupCreator(W64, device=local, sha1=True, timing=True)
