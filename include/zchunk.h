@@ -205,6 +205,14 @@ int zc_lzo_compress(zc_ctx* ctx, const void* d_payload, const uint64_t* pay_off,
  * batch of them) without device buffers of its own */
 int zc_lzo_compress_host(zc_ctx* ctx, const void* payload, const uint64_t* pay_off, const uint64_t* pay_size,
                          size_t n, void* out, const uint64_t* out_off, uint64_t* out_size);
+/* Adler-32 (zlib's adler32 from its initial value 1, as Adler32 wraps it: adler32.hh:13-33) of
+ * each device range d_base[off[i] ..+ len[i]) -> out[i] (host).  EncryptedFile::OutputStream
+ * keeps one running Adler-32 over everything a bundle file holds and writes it after the
+ * BundleInfo and after the payload (encrypted_file.cc:248-300,336-340, bundle.cc:116,153):
+ * the payload's share comes from here, joined to the running value with zlib's
+ * adler32_combine(running, out[i], len[i]). */
+int zc_adler32(zc_ctx* ctx, const void* d_base, const uint64_t* off, const uint64_t* len, size_t n,
+               uint32_t* out);
 /* device time of the last zc_lzo_compress's parse kernel (ms) and its 48 KiB blocks */
 int zc_lzo_last_stats(const zc_ctx* ctx, double* parse_ms, uint64_t* blocks);
 

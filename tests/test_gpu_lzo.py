@@ -155,3 +155,32 @@ def test_bundles_of_a_chunked_stream(torch_cuda, comp, spec_kind):
                       for m in members)
         got = out[int(out_off[b]):int(out_off[b]) + int(out_size[b])].tobytes()
         assert got == lzo_oracle.frame(pl), f"bundle {b}"
+
+
+def test_adler32_of_device_ranges(torch_cuda, comp):
+    """zc_adler32 == zlib.adler32 (the library Adler32 wraps, adler32.hh) for
+    ranges of every alignment and length, incl. empty, a few bytes inside one
+    16-byte slot, and a 96 MiB range; and of framed bundle outputs."""
+    import zlib
+    rng = np.random.default_rng(6)
+    host = rng.integers(0, 256, 100 << 20, dtype=np.uint8)
+    host[5 << 20:7 << 20] = 0xFF  # long runs of the largest byte (the sums' worst case)
+    d = torch_cuda.from_numpy(host).cuda()
+    offs, lens = [], []
+    for ln in [0, 1, 2, 3, 15, 16, 17, 31, 33, 255, 4096, 65537, 2097152, 3000001]:
+        for _ in range(3):
+            o = int(rng.integers(0, len(host) - ln - 1))
+            offs.append(o)
+            lens.append(ln)
+    offs += [3, 5 << 20, 0]
+    lens += [12, 2 << 20, 96 << 20]
+    got = comp.adler32(d.data_ptr() + 1, offs, lens)  # an unaligned base pointer: range = host[o + 1 ..]
+    for o, ln, g in zip(offs, lens, got):
+        assert int(g) == zlib.adler32(host[o + 1:o + 1 + ln].tobytes()), (o, ln)
+    payloads = [payload(k, 300000 + 7 * i, 500 + i) for i, k in enumerate(KINDS)]
+    framed = _compress(torch_cuda, comp, payloads, rng)
+    blob = np.frombuffer(b"".join(framed), dtype=np.uint8)
+    dd = torch_cuda.from_numpy(blob.copy()).cuda()
+    fo = np.concatenate([[0], np.cumsum([len(f) for f in framed])[:-1]])
+    got = comp.adler32(dd.data_ptr(), fo, [len(f) for f in framed])
+    assert [int(g) for g in got] == [zlib.adler32(f) for f in framed]

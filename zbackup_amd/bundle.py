@@ -86,6 +86,14 @@ class BundleCompressor:
         _check(self._L, self._ctx, rc, "zc_lzo_compress_host")
         return [out[int(o):int(o) + int(s)].tobytes() for o, s in zip(out_off, out_size)]
 
+    def adler32(self, d_base, off, length):
+        """zlib adler32 (from 1) of each device range d_base[off[i] ..+ length[i])."""
+        off, length = _u64(off), _u64(length)
+        out = np.zeros(len(off), dtype=np.uint32)
+        rc = self._L.zc_adler32(self._ctx, d_base, off.ctypes.data, length.ctypes.data, len(off), out.ctypes.data)
+        _check(self._L, self._ctx, rc, "zc_adler32")
+        return out
+
     def last_stats(self):
         """(parse kernel ms, 48 KiB blocks) of the last compress()."""
         ms, blocks = ctypes.c_double(), ctypes.c_uint64()

@@ -332,6 +332,9 @@ const LzoTimes* lzo_times(const LzoScratch* s);
 // d_dst <- d_src[off[i] ..+ size[i]) for i = 0 .. n-1, back to back
 hipError_t lzo_gather(LzoScratch* s, const uint8_t* d_src, const uint64_t* off, const uint64_t* size, size_t n,
                       uint8_t* d_dst, hipStream_t st);
+// zlib adler32 (from 1) of each range d_base[off[i] ..+ len[i]) -> out (host)
+hipError_t lzo_adler32(LzoScratch* s, const uint8_t* d_base, const uint64_t* off, const uint64_t* len, size_t n,
+                       uint32_t* out, hipStream_t st);
 // payload i = d_payload[pay_off[i] ..+ pay_size[i]) -> framed lzo1x_1 output at
 // d_out + out_off[i]; out_size (host) receives the framed sizes
 hipError_t lzo_compress(LzoScratch* s, const uint8_t* d_payload, const uint64_t* pay_off, const uint64_t* pay_size,

@@ -2691,6 +2691,22 @@ int zc_lzo_compress_host(zc_ctx* c, const void* payload, const uint64_t* pay_off
   });
 }
 
+int zc_adler32(zc_ctx* c, const void* d_base, const uint64_t* off, const uint64_t* len, size_t n, uint32_t* out) {
+  if (!c || (n && (!d_base || !off || !len || !out))) return ZC_ERR_ARG;
+  if (!n) return ZC_OK;
+  DeviceGuard g(c->device);
+  if (!c->lzo) c->lzo = lzo_scratch_new();
+  hipError_t e = hipEventRecord(c->ev_in, nullptr);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+  if (e == hipSuccess) e = lzo_adler32(c->lzo, (const uint8_t*)d_base, off, len, n, out, c->stream);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);
+    return lzo_fail(c, e, "zc_adler32");
+  }
+  c->err.clear();
+  return ZC_OK;
+}
+
 int zc_lzo_last_stats(const zc_ctx* c, double* parse_ms, uint64_t* blocks) {
   if (!c) return ZC_ERR_ARG;
   const LzoTimes t = c->lzo ? *lzo_times(c->lzo) : LzoTimes{};

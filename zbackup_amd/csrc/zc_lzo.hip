@@ -133,6 +133,69 @@ __global__ void zc_lzo_or_kernel(uint8_t* out, const uint64_t* or_at, const uint
   if (i < nb && or_val[i]) out[or_at[i]] |= (uint8_t)or_val[i];
 }
 
+// Adler-32 (zlib's, as Adler32 wraps it: adler32.hh:13-33) of one range per
+// 256-thread block, from the initial value 1: a = 1 + sum b_i, b = n + sum
+// (n - i) b_i (mod 65521) = n + n * S1 - sum i b_i.  Thread t takes the
+// 16-byte slots t, t + 256, ... of the 16-byte grid over the range (bytes
+// outside it masked), accumulating S1 and sum (i mod 65521) b_i exactly in 64
+// bits; the block sums them and reduces once.
+constexpr uint32_t kAdlerMod = 65521;
+__global__ __launch_bounds__(256) void zc_adler32_kernel(const uint8_t* __restrict__ base,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint64_t* __restrict__ len, uint32_t* __restrict__ out) {
+  __shared__ uint64_t red[2][256];
+  const uint64_t n = len[blockIdx.x];
+  const uint64_t a0 = (uint64_t)(uintptr_t)(base + off[blockIdx.x]);  // absolute address
+  const uint64_t g0 = a0 & ~15ull;                   // its 16-byte slot: never crosses a page
+  const uint64_t nslot = (a0 + n + 15 - g0) >> 4;     // slots touching the range
+  uint64_t s1 = 0, si = 0;
+  for (uint64_t k = threadIdx.x; k < nslot && n; k += 256) {
+    const uint64_t q = g0 + 16 * k;                   // the slot's address
+    u32x4 v = *reinterpret_cast<const u32x4*>((uintptr_t)q);
+    const uint32_t w[4] = {v[0], v[1], v[2], v[3]};
+    // position of the slot's byte 0 in the range (may be "negative" for the
+    // head slot: those bytes are masked); congruent mod 65521 is enough
+    const int64_t p0 = (int64_t)q - (int64_t)a0;
+    const bool full = p0 >= 0 && (uint64_t)p0 + 16 <= n;
+    uint32_t bs = 0, bk = 0;  // sum of bytes, sum of j * byte (j = byte index in the slot)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t x = w[d];
+      if (!full) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t p = p0 + 4 * d + j;
+          if (p >= 0 && (uint64_t)p < n) m |= 0xFFu << (8 * j);
+        }
+        x &= m;
+      }
+      bs = __builtin_amdgcn_udot4(x, 0x01010101u, bs, false);
+      bk = __builtin_amdgcn_udot4(x, (uint32_t)((4 * d) | (4 * d + 1) << 8 | (4 * d + 2) << 16 | (4 * d + 3) << 24),
+                                  bk, false);
+    }
+    const uint64_t pm = (uint64_t)((p0 % (int64_t)kAdlerMod + kAdlerMod) % kAdlerMod);
+    s1 += bs;
+    si += pm * bs + bk;
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = si;
+  __syncthreads();
+  for (uint32_t h = 128; h; h >>= 1) {
+    if (threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] += red[1][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const uint64_t S1 = red[0][0] % kAdlerMod, SI = red[1][0] % kAdlerMod, nm = n % kAdlerMod;
+    const uint32_t a = (uint32_t)((1 + S1) % kAdlerMod);
+    const uint32_t b = (uint32_t)((nm + nm * S1 % kAdlerMod + kAdlerMod - SI) % kAdlerMod);
+    out[blockIdx.x] = b << 16 | a;
+  }
+}
+
 template <class T>
 struct Buf {
   T* p = nullptr;
@@ -170,6 +233,8 @@ constexpr uint32_t kMaxBatchBlocks = 1u << 18;
 
 struct LzoScratch {
   Buf<uint32_t> dict;
+  Buf<uint64_t> ad_off, ad_len;
+  Buf<uint32_t> ad_out;
   Buf<uint8_t> stage;
   Buf<BlkOut> bo;
   Buf<BlkDesc> blks;
@@ -213,6 +278,21 @@ hipError_t lzo_gather(LzoScratch* s, const uint8_t* d_src, const uint64_t* off, 
     pos += size[i];
   }
   return lzo_copy_list(s, list, st);
+}
+
+hipError_t lzo_adler32(LzoScratch* s, const uint8_t* d_base, const uint64_t* off, const uint64_t* len, size_t n,
+                       uint32_t* out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  LCK(s->ad_off.ensure(n));
+  LCK(s->ad_len.ensure(n));
+  LCK(s->ad_out.ensure(n));
+  LCK(hipMemcpyAsync(s->ad_off.p, off, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  LCK(hipMemcpyAsync(s->ad_len.p, len, n * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(zc_adler32_kernel, dim3((uint32_t)n), dim3(256), 0, st, d_base, s->ad_off.p, s->ad_len.p,
+                     s->ad_out.p);
+  LCK(hipGetLastError());
+  LCK(hipMemcpyAsync(out, s->ad_out.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  return hipStreamSynchronize(st);
 }
 
 static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint64_t* pay_off,
