@@ -26,11 +26,10 @@ int main(int argc, char** argv) {
   constexpr int P = kScanProduct;
   std::vector<V> vs = {
     {"product (nt DMA)", zc_scan_kernel<P>, {}},
+    {"no_atomic", zc_scan_kernel<P | ABL_NO_ATOMIC>, {}},
     {"te_no_anchor_store", zc_scan_kernel<P | ABL_TE_NO_ANCHOR_STORE>, {}},
     {"te_digest_only", zc_scan_kernel<P | ABL_TE_DIGEST_ONLY>, {}},
-    {"full_te_no_store", zc_scan_kernel<P | ABL_TE_NO_STORE>, {}},
-    {"stage_only", zc_scan_kernel<P | ABL_NO_BYTES>, {}},
-    {"stage_only_te_no_store", zc_scan_kernel<P | ABL_NO_BYTES | ABL_TE_NO_STORE>, {}},
+    {"te_no_store", zc_scan_kernel<P | ABL_TE_NO_STORE>, {}},
   };
   for (int round = 0; round < 12; ++round)
     for (auto& v : vs) {

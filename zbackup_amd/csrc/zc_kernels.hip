@@ -205,7 +205,8 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
 enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
        ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128, ABL_TE_DIGEST_ONLY = 256,
        ABL_DMA_NT = 512, ABL_DMA_SC1 = 1024, ABL_STAGGER_HALF = 2048, ABL_STAGGER_QUARTER = 4096,
-       ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768 };
+       ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768,
+       ABL_TE_DIGEST_NT = 65536, ABL_TE_DIGEST_SAME = 131072 };
 // the product's scan: the staging DMA is non-temporal (the stream is read
 // once; tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB)
 constexpr int kScanProduct = ABL_DMA_NT;
@@ -552,7 +553,7 @@ template <int ABL>
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
                                                   const uint64_t (&bk)[kDigests], const WaveList& wl,
                                                   uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
-                                                  unsigned long long* __restrict__ counters) {
+                                                  uint32_t& acc_pool, uint32_t& acc_over) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
   if (ABL & ABL_TE_NO_STORE) {
     uint32_t x = 0;
@@ -561,10 +562,16 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
     asm volatile("" ::"v"(x));
     return 0;
   }
+  if (ABL & ABL_TE_DIGEST_SAME) bo = (uint4*)(blk + (span0 % ZC_STILE) / ZC_SPAN);  // timing only: L2-hot
 #pragma unroll
-  for (int t = 0; t < kDigests / 2; ++t)
-    bo[t] = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
-                       (uint32_t)(bk[2 * t + 1] >> 32));
+  for (int t = 0; t < kDigests / 2; ++t) {
+    const uint4 v = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
+                               (uint32_t)(bk[2 * t + 1] >> 32));
+    if (ABL & ABL_TE_DIGEST_NT)
+      __builtin_nontemporal_store(*(const v4u32*)&v, (v4u32*)(bo + t));
+    else
+      bo[t] = v;
+  }
   if (ABL & ABL_TE_DIGEST_ONLY) return kDigests / 2;
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)(wt - po.wt0) * po.wcap;
@@ -637,9 +644,12 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   if (lane == 0) {
     po.base[wt] = base;
     po.cnt[wt] = over ? ZC_WT_OVERFLOW : tot;
-    if (!(ABL & ABL_NO_ATOMIC)) atomicAdd(&counters[over ? CNT_OVERFLOW : CNT_POOL], over ? 1ull : (unsigned long long)tot);
   }
-  return kDigests / 2 + __builtin_amdgcn_readfirstlane(nst) + 2 + ((ABL & ABL_NO_ATOMIC) ? 0 : 1);
+  // the pool / overflow counters are added once per wave at the kernel's end
+  // (one same-address atomic per wave-tile serialised in L2: 1.5 % of the scan)
+  acc_pool += over ? 0u : tot;
+  acc_over += over ? 1u : 0u;
+  return kDigests / 2 + __builtin_amdgcn_readfirstlane(nst) + 2;
 }
 
 // The workgroup's rounds form one flat sequence over its tiles (32 per
@@ -702,6 +712,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   uint64_t span0 = 0;
   uint32_t tail_stores = 0;  // global stores the last tile end left in flight
   uint32_t last = kNoEntry;  // this lane's newest entry in the wave's list
+  uint32_t acc_pool = 0, acc_over = 0;  // wave-uniform: anchors stored, wave-tiles overflowed
 
 #pragma unroll 1
   for (uint32_t R = 0; R < nR; ++R) {
@@ -763,7 +774,11 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (tile_end) tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, counters);
+    if (tile_end) tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
+  }
+  if (!(ABL & ABL_NO_ATOMIC) && lane == 0) {
+    if (acc_pool) atomicAdd(&counters[CNT_POOL], (unsigned long long)acc_pool);
+    if (acc_over) atomicAdd(&counters[CNT_OVERFLOW], (unsigned long long)acc_over);
   }
 }
 
