@@ -200,7 +200,9 @@ template <class T>
 struct Buf {
   T* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t n, bool zero = false) {
+  // grow to n elements; *fresh (if given) reports a new allocation
+  hipError_t ensure(size_t n, bool* fresh = nullptr) {
+    if (fresh) *fresh = false;
     if (n <= cap && p) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -211,8 +213,8 @@ struct Buf {
       return e;
     }
     cap = n;
-    if (zero) e = hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(T));
-    return e;
+    if (fresh) *fresh = true;
+    return hipSuccess;
   }
   ~Buf() {
     if (p) (void)hipFree(p);
@@ -315,10 +317,11 @@ static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint6
   const uint32_t nblk = (uint32_t)blks.size(), nb = (uint32_t)bund.size();
   // dictionaries: entries of an earlier generation read as empty; zeroed
   // when (re)allocated and when the 16-bit generation wraps
-  if (s->dict.cap < (size_t)nblk * kDictSize) {
-    LCK(s->dict.ensure((size_t)nblk * kDictSize, true));
-    s->gen = 0;
-  } else if (s->gen == 0xffff) {
+  // (the clear is queued on the call's stream, ahead of the parse: the
+  // context's streams are non-blocking, so a null-stream memset would not be)
+  bool fresh = false;
+  LCK(s->dict.ensure((size_t)nblk * kDictSize, &fresh));
+  if (fresh || s->gen == 0xffff) {
     LCK(hipMemsetAsync(s->dict.p, 0, s->dict.cap * sizeof(uint32_t), st));
     s->gen = 0;
   }
