@@ -212,7 +212,8 @@ enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, 
 constexpr int kScanProduct = ABL_DMA_NT;
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
-  uint32_t* e;      // {(rel of the piece >> 4) << 8 | the lane's previous entry, gear before the piece}
+  uint32_t* e;      // {the lane's previous entry | (rel of the piece >> 4) << 8 | lane << 16, gear before
+                    //  the piece, tile-end scratch: anchor mask | pool offset << 16}
   uint4* x;         // the piece's 16 bytes
   uint32_t n;       // wave-uniform count (may exceed capacity: then rescan)
 };
@@ -290,8 +291,8 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
     }
     const uint32_t idx = wl.n + lane_prefix(any);
     if (m >= lo_thr && idx < ZC_WLIST) {
-      wl.e[2 * idx] = ((rel >> 4) << 8) | last;
-      wl.e[2 * idx + 1] = g0;
+      wl.e[3 * idx] = ((rel >> 4) << 8) | last | (__lane_id() << 16);
+      wl.e[3 * idx + 1] = g0;
       wl.x[idx] = v;
       last = idx;
     }
@@ -513,9 +514,9 @@ struct PieceHits {
 
 __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, uint64_t span0, int32_t lo_thr) {
   PieceHits h;
-  const uint32_t e0 = wl.e[2 * i];
+  const uint32_t e0 = wl.e[3 * i];
   h.rel = ((e0 >> 8) & 0xFFu) << 4;
-  h.g0 = wl.e[2 * i + 1];
+  h.g0 = wl.e[3 * i + 1];
   const uint4 v = wl.x[i];
   h.xs[0] = v.x;
   h.xs[1] = v.y;
@@ -578,47 +579,62 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   uint32_t tot = 0, excl = 0, nst = 0;
   bool over = wl.n > ZC_WLIST;
   if (!over) {
+    const uint32_t ne = wl.n;  // <= ZC_WLIST
+    const uint64_t tspan0 = span0 - (uint64_t)lane * ZC_LSPAN;  // the wave-tile's first byte
+    // pass 1, over the entries (one per lane per step): each piece's anchor
+    // mask, re-derived from its bytes and the gear before it
+    for (uint32_t i = lane; i < ne; i += 64) {
+      const uint32_t L = (wl.e[3 * i] >> 16) & 63u;
+      wl.e[3 * i + 2] = piece_hits(wl, i, tspan0 + (uint64_t)L * ZC_LSPAN, lo_thr).mask;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // pass 2, along each lane's own chain (newest entry first): its counts,
+    // the wave's prefix sum, then each entry's pool offset -- within each half
+    // (either half may be the one taken first), so the wave-tile's anchors
+    // land in position order
     uint32_t cnt = 0, cnt_lo = 0;  // cnt_lo: anchors in the span's first half
-    for (uint32_t i = last; i != kNoEntry; i = wl.e[2 * i] & 0xFFu) {
-      const PieceHits h = piece_hits(wl, i, span0, lo_thr);
-      wl.e[2 * i] = (wl.e[2 * i] & 0xFFFFu) | (h.mask << 16);
-      cnt += __popc(h.mask);
-      if (h.rel < kHalfSpan) cnt_lo += __popc(h.mask);
+    for (uint32_t i = last; i != kNoEntry; i = wl.e[3 * i] & 0xFFu) {
+      const uint32_t c = __popc(wl.e[3 * i + 2]);
+      cnt += c;
+      if ((((wl.e[3 * i] >> 8) & 0xFFu) << 4) < kHalfSpan) cnt_lo += c;
     }
     excl = wave_excl_scan(cnt, lane, &tot);
     over = tot > po.wcap;
     if (!over) {
-      // newest entry first, within each half: the first half's anchors end at
-      // excl + cnt_lo, the second half's at excl + cnt (either half may be the
-      // one taken first)
-      const uint32_t sbase = lane * ZC_LSPAN;  // offset of the span in the wave-tile
       uint32_t k_lo = excl + cnt_lo, k_hi = excl + cnt;
-      // one wave-uniform loop, one anchor per lane per pass, so the store
-      // instructions issued are counted exactly (nst): the next tile's first
-      // wait then leaves exactly them in flight instead of draining the
-      // round prefetched behind them
-      uint32_t i = last, mask = 0, w = 0, rel = 0;
+      for (uint32_t i = last; i != kNoEntry; i = wl.e[3 * i] & 0xFFu) {
+        const uint32_t m = wl.e[3 * i + 2];
+        uint32_t& k = ((((wl.e[3 * i] >> 8) & 0xFFu) << 4) < kHalfSpan) ? k_lo : k_hi;
+        k -= __popc(m);
+        wl.e[3 * i + 2] = m | (k << 16);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      // pass 3, over the entries again: the stores, in one wave-uniform loop
+      // (one anchor per lane per pass) whose store instructions are counted
+      // exactly (nst): the next tile's first wait then leaves exactly them in
+      // flight instead of draining the round prefetched behind them
+      uint32_t i = lane, mask = 0, w = 0, sb = 0;
       uint32_t xs[4] = {0, 0, 0, 0}, gd[4] = {0, 0, 0, 0};
       for (;;) {
         // a lane whose entry is used up takes its next one (an entry's mask
         // may be empty: the stream's first positions are no anchors)
-        while (!mask && i != kNoEntry) {
-          const uint32_t e0 = wl.e[2 * i];
-          rel = ((e0 >> 8) & 0xFFu) << 4;
-          mask = e0 >> 16;
+        while (!mask && i < ne) {
+          const uint32_t e0 = wl.e[3 * i], e2 = wl.e[3 * i + 2];
+          mask = e2 & 0xFFFFu;
+          w = e2 >> 16;
+          sb = ((e0 >> 16) & 63u) * ZC_LSPAN + (((e0 >> 8) & 0xFFu) << 4);  // in the wave-tile
           const uint4 v = wl.x[i];
           xs[0] = v.x;
           xs[1] = v.y;
           xs[2] = v.z;
           xs[3] = v.w;
           // the gear before each dword of the piece
-          gd[0] = wl.e[2 * i + 1];
+          gd[0] = wl.e[3 * i + 1];
 #pragma unroll
           for (int d = 0; d < 3; ++d) gd[d + 1] = (gd[d] << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
-          uint32_t& k = rel < kHalfSpan ? k_lo : k_hi;
-          k -= __popc(mask);
-          w = k;
-          i = e0 & 0xFFu;
+          i += 64;
         }
         if (__ballot(mask != 0) == 0) break;
         if (ABL & ABL_TE_NO_ANCHOR_STORE) {
@@ -632,7 +648,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
           // g at position t: the dword's gear shifted q + 1, plus its first q + 1
           // bytes weighted 2^(q - j)
           const uint32_t g = (gdd << (q + 1)) + __builtin_amdgcn_udot4(xd, 0x01020408u >> (8 * (3 - q)), 0u, false);
-          po.rel[base + w] = sbase + rel + t;
+          po.rel[base + w] = sb + t;
           po.g[base + w] = g;
           mask &= mask - 1;
           ++w;
@@ -664,7 +680,7 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
-  __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 2];
+  __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 3];
   __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
   constexpr uint32_t kRpt = kRounds;  // rounds per tile
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
