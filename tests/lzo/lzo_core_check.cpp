@@ -112,8 +112,9 @@ static std::vector<uint8_t> make_input(uint64_t seed, size_t n, int kind) {
 int main(int argc, char** argv) {
   if (lzo_init() != LZO_E_OK) return 3;
   int cases = argc > 1 ? atoi(argv[1]) : 400;
-  const size_t sizes[] = {0, 1, 3, 4, 17, 20, 21, 22, 40, 41, 100, 1000, 49151, 49152, 49153, 49172, 49173,
-                          49174, 98304, 98324, 98325, 100000, 262144, 2097152};
+  const size_t sizes[] = {0, 1, 3, 4, 17, 20, 21, 22, 27, 29, 31, 32, 33, 40, 41, 100, 1000, 49151, 49152, 49153,
+                          49172, 49173, 49174, 49175, 49180, 49183, 49184, 98304, 98324, 98325, 98335, 100000,
+                          262144, 2097152};
   int n_ok = 0;
   for (int c = 0; c < cases; c++) {
     size_t n = c < (int)(sizeof(sizes) / sizeof(sizes[0])) * 6 ? sizes[c / 6] : (size_t)(std::mt19937_64(c)() % 3000000);
@@ -130,6 +131,17 @@ int main(int argc, char** argv) {
     }
     n_ok++;
   }
+  // every length up to 160 and every short last block (49152 + 21 .. 63), all kinds
+  for (int kind = 0; kind < 6; kind++)
+    for (size_t n = 0; n <= 160 + 43; n++) {
+      const size_t len = n <= 160 ? n : 49152 + 21 + (n - 161);
+      auto in = make_input(90000 + 1000 * kind + n, len, kind);
+      if (lzo_compress(in.data(), len) != core_compress(in.data(), len)) {
+        printf("MISMATCH kind %d n %zu\n", kind, len);
+        return 1;
+      }
+      n_ok++;
+    }
   printf("ok %d\n", n_ok);
   return 0;
 }

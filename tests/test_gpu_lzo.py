@@ -184,3 +184,13 @@ def test_adler32_of_device_ranges(torch_cuda, comp):
     fo = np.concatenate([[0], np.cumsum([len(f) for f in framed])[:-1]])
     got = comp.adler32(dd.data_ptr(), fo, [len(f) for f in framed])
     assert [int(g) for g in got] == [zlib.adler32(f) for f in framed]
+
+
+def test_lzo_many_tiny_bundles(torch_cuda, comp):
+    """5,000 payloads of 0-300 bytes in one call (bundles below one 48 KiB
+    block, at and around the 20/21-byte edge, most without any match)."""
+    rng = np.random.default_rng(7)
+    sizes = rng.integers(0, 300, 5000)
+    sizes[:64] = np.arange(64)
+    payloads = [payload(KINDS[i % len(KINDS)], int(n), 700 + i) for i, n in enumerate(sizes)]
+    _check(payloads, _compress(torch_cuda, comp, payloads, rng))

@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
     {"te_digest_only", zc_scan_kernel<P | ABL_TE_DIGEST_ONLY>, {}},
     {"te_no_store", zc_scan_kernel<P | ABL_TE_NO_STORE>, {}},
   };
-  for (int round = 0; round < 12; ++round)
+  for (int round = 0; round < 25; ++round)
     for (auto& v : vs) {
       CK(hipMemset(cnt, 0, 64));
       CK(hipEventRecord(a));

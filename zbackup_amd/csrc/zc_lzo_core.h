@@ -17,7 +17,11 @@
 // match (the match extension stops short of the block's end - 20), and a
 // block without one passes on ti + its length, so every block but a payload's
 // first starts with ti >= 4: its parse does not depend on the blocks before
-// it.  Each block is therefore parsed on its own lane (the first with ti = 0)
+// it.  (One more rule of the block loop: a block whose length plus the
+// pending literals is under 32 bytes is not parsed at all -- a side effect of
+// the loop's pointer-overflow guard -- which only a payload of 21-31 bytes or
+// a short last block can meet; chain_bundle applies it.)  Each block is
+// therefore parsed on its own lane (the first with ti = 0)
 // and encodes itself into a staging area — everything from its first match
 // on; the first literal run's header and bytes (which include the inherited
 // ti literals) are written by a per-bundle assembly pass (chain_bundle) that
@@ -240,6 +244,11 @@ ZC_HD inline uint64_t chain_bundle(uint64_t n, const BlkOut* bo, uint8_t* out, C
   *or_val = 0;
   while (rem > 20) {
     const uint32_t ll = rem < kBlock ? (uint32_t)rem : kBlock;
+    // DO_COMPRESS's overflow guard `(ll_end + ((t + ll) >> 5)) <= ll_end` also
+    // holds when the pending literals and the block are under 32 bytes: the
+    // block is not parsed and everything left is literals (only a payload of
+    // 21-31 bytes, or a short last block, meets it; its parse is ignored)
+    if (((ti + ll) >> 5) == 0) break;
     const BlkOut o = bo[k];
     if (o.ntok) {
       const uint64_t L0 = ti + o.lit0;
