@@ -194,3 +194,14 @@ def test_lzo_many_tiny_bundles(torch_cuda, comp):
     sizes[:64] = np.arange(64)
     payloads = [payload(KINDS[i % len(KINDS)], int(n), 700 + i) for i, n in enumerate(sizes)]
     _check(payloads, _compress(torch_cuda, comp, payloads, rng))
+
+
+def test_lzo_short_last_blocks_and_random_sweep(torch_cuda, comp):
+    """Every short last block (49152 * k + 21 .. 40, k = 1, 2) for every kind,
+    and 300 payloads of random size up to 200 KB: the block loop's guard on
+    short blocks, with the pending literals the full blocks leave."""
+    rng = np.random.default_rng(8)
+    payloads = [payload(kind, 49152 * k + r, 800 + 100 * k + r + 1000 * i)
+                for i, kind in enumerate(KINDS) for k in (1, 2) for r in range(21, 41)]
+    payloads += [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 200000)), 5000 + i) for i in range(300)]
+    _check(payloads, _compress(torch_cuda, comp, payloads, rng))
