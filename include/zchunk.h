@@ -161,6 +161,13 @@ int zc_forget_stream_chunks(zc_ctx* ctx);
  * (the payload of BYTES records, for serializing bytes_to_emit, and of NEW
  * chunks, for Writer::add); for a fed stream, the bytes still in its window */
 int zc_read_stream(const zc_ctx* ctx, uint64_t offset, size_t n, void* host_out);
+/* the records' BackupInstruction stream, as BackupCreator::outputInstruction writes it
+ * (Message::serialize, message.cc:16-23: varint32 length + field 1 chunk_to_emit =
+ * ChunkId::toBlob (chunk_id.cc:19-27) | field 2 bytes_to_emit, the record's bytes read from
+ * the last stream as zc_read_stream does): n records into out (cap bytes); *n_out = the bytes
+ * written, or needed (ZC_ERR_ARG) when cap is too small */
+int zc_serialize_records(const zc_ctx* ctx, const zc_record* recs, size_t n, void* out, size_t cap,
+                         size_t* n_out);
 const char* zc_last_error(const zc_ctx* ctx);
 
 /* synthetic seeded stream on the device (tests / benchmarks): byte k is byte

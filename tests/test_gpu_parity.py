@@ -242,9 +242,13 @@ def test_forget_stream_chunks_restores_the_seeded_index(torch_cuda):
             bc.forget_stream_chunks()
 
 
-def test_get_backup_data_matches_oracle_serialization(torch_cuda):
+@pytest.mark.parametrize("name,path", [("frag50", "feed"), ("frag50", "device"), ("mixed", "feed"),
+                                       ("mixed", "device"), ("small_tail", "window")])
+def test_get_backup_data_matches_oracle_serialization(torch_cuda, name, path):
+    # zc_serialize_records (Message::serialize per record, bytes_to_emit read
+    # from the stream) vs the same stream serialized from the oracle's records
     from zbackup_amd import BackupCreator, chunk_id_blob, serialize_instruction
-    meta, seeds, want = _case("frag50")
+    meta, seeds, want = _case(name)
     data = oracle.gen(meta["spec"])
     expect = b""
     for (k, off, size, h, sha) in want:
@@ -252,9 +256,13 @@ def test_get_backup_data_matches_oracle_serialization(torch_cuda):
             expect += serialize_instruction(raw=data[off:off + size].tobytes())
         else:
             expect += serialize_instruction(chunk_blob=chunk_id_blob(bytes.fromhex(sha), h))
-    with BackupCreator(meta["W"]) as bc:
-        bc.feed(data)
-        bc.finish()
+    with BackupCreator(meta["W"], seeds=seeds, window=(8 * meta["W"] + (16 << 20)) if path == "window" else None) as bc:
+        if path == "device":
+            t = torch_cuda.from_numpy(data).to("cuda")
+            bc.chunk_device(t.data_ptr(), data.size)
+        else:
+            bc.feed(data)
+            bc.finish()
         assert bc.get_backup_data() == expect
         with pytest.raises(Exception):
             bc.get_backup_data()  # backup_creator.cc:277 CHECK: only once

@@ -159,13 +159,14 @@ class BackupCreator:
         if self._data_taken:
             raise _lib.ZcError("getBackupData() called twice")
         self._data_taken = True
-        out = bytearray()
-        for r in self.records():
-            if r["kind"] == _lib.ZC_BYTES:
-                out += serialize_instruction(raw=self.read_stream(int(r["offset"]), int(r["size"])))
-            else:
-                out += serialize_instruction(chunk_blob=chunk_id_blob(r["sha1"], int(r["rolling"])))
-        return bytes(out)
+        recs = np.ascontiguousarray(self.records())
+        need = ctypes.c_size_t()
+        self._L.zc_serialize_records(self._ctx, recs.ctypes.data, len(recs), None, 0, ctypes.byref(need))
+        out = np.zeros(max(need.value, 1), dtype=np.uint8)
+        rc = self._L.zc_serialize_records(self._ctx, recs.ctypes.data, len(recs), out.ctypes.data, out.size,
+                                          ctypes.byref(need))
+        _check(self._L, self._ctx, rc, "zc_serialize_records")
+        return out[:need.value].tobytes()
 
     def stats(self):
         st = _lib.ZcStats()

@@ -2574,6 +2574,56 @@ int zc_read_stream(const zc_ctx* c, uint64_t offset, size_t n, void* host_out) {
   return e == hipSuccess ? ZC_OK : ZC_ERR_HIP;
 }
 
+// Message::serialize of BackupInstruction (message.cc:16-23, zbackup.proto:149-159): a
+// varint32 length, then field 1 (chunk_to_emit: ChunkId::toBlob, chunk_id.cc:19-27) or field
+// 2 (bytes_to_emit), each a tag byte, a varint length and the bytes
+static size_t varint_len(uint64_t v) {
+  size_t k = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    ++k;
+  }
+  return k;
+}
+static uint8_t* put_varint(uint8_t* p, uint64_t v) {
+  while (v >= 0x80) {
+    *p++ = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  *p++ = (uint8_t)v;
+  return p;
+}
+
+int zc_serialize_records(const zc_ctx* c, const zc_record* recs, size_t n, void* out, size_t cap, size_t* n_out) {
+  if (!c || (n && !recs) || !n_out || (cap && !out)) return ZC_ERR_ARG;
+  size_t need = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t len = recs[i].kind == ZC_BYTES ? recs[i].size : 24;
+    const uint64_t body = 1 + varint_len(len) + len;
+    need += varint_len(body) + body;
+  }
+  *n_out = need;
+  if (need > cap) return ZC_ERR_ARG;  // *n_out: the bytes needed
+  uint8_t* p = (uint8_t*)out;
+  for (size_t i = 0; i < n; ++i) {
+    const zc_record& r = recs[i];
+    const bool raw = r.kind == ZC_BYTES;
+    const uint64_t len = raw ? r.size : 24;
+    p = put_varint(p, 1 + varint_len(len) + len);
+    *p++ = raw ? 0x12 : 0x0a;
+    p = put_varint(p, len);
+    if (raw) {
+      const int rc = zc_read_stream(c, r.offset, r.size, p);  // the bytes of bytes_to_emit
+      if (rc != ZC_OK) return rc;
+    } else {
+      memcpy(p, r.sha1, 16);  // ChunkId::toBlob: SHA-1 prefix, then the rolling hash LE
+      for (int k = 0; k < 8; ++k) p[16 + k] = (uint8_t)(r.rolling >> (8 * k));
+    }
+    p += len;
+  }
+  return ZC_OK;
+}
+
 const char* zc_last_error(const zc_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int zc_fill_splitmix64(void* d_data, uint64_t n, uint64_t seed, int device) {
