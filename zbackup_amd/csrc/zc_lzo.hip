@@ -119,7 +119,16 @@ __global__ __launch_bounds__(256) void zc_lzo_copy_kernel(const Copy* __restrict
   dst += head;
   len -= head;
   const uint64_t nv = len >> 4;
-  for (uint64_t v = lane; v < nv; v += 64) {
+  uint64_t v = lane;
+  // four 16-byte loads in flight per lane before their stores
+  for (; v + 3 * 64 < nv; v += 4 * 64) {
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_memcpy(&x[u], src + (v + u * 64) * 16, 16);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(x[u], reinterpret_cast<u32x4*>(dst + (v + u * 64) * 16));
+  }
+  for (; v < nv; v += 64) {
     u32x4 x;
     __builtin_memcpy(&x, src + v * 16, 16);
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst + v * 16));
