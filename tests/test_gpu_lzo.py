@@ -205,3 +205,13 @@ def test_lzo_short_last_blocks_and_random_sweep(torch_cuda, comp):
                 for i, kind in enumerate(KINDS) for k in (1, 2) for r in range(21, 41)]
     payloads += [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 200000)), 5000 + i) for i in range(300)]
     _check(payloads, _compress(torch_cuda, comp, payloads, rng))
+
+
+def test_lzo_call_split_into_batches(torch_cuda, comp, monkeypatch):
+    """A call larger than one device batch (normally 2^18 blocks = 12 GiB)
+    runs batch after batch, each a new dictionary generation: here batches of
+    at most 5 blocks (ZC_LZO_BATCH_BLOCKS), payloads of 0-400 KB."""
+    monkeypatch.setenv("ZC_LZO_BATCH_BLOCKS", "5")
+    rng = np.random.default_rng(9)
+    payloads = [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 400000)), 900 + i) for i in range(40)]
+    _check(payloads, _compress(torch_cuda, comp, payloads, rng))

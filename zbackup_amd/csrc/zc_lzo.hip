@@ -20,6 +20,8 @@
 // The same copy kernel gathers chunk extents into bundle payloads.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -237,8 +239,14 @@ struct Buf {
   } while (0)
 
 // at most this many blocks per device batch (12 GiB of payload; the
-// dictionaries take 64 KiB and the staging 51 KiB per block)
+// dictionaries take 64 KiB and the staging 51 KiB per block); the environment
+// variable ZC_LZO_BATCH_BLOCKS lowers it (tests: a call split into batches)
 constexpr uint32_t kMaxBatchBlocks = 1u << 18;
+uint32_t max_batch_blocks() {
+  const char* e = getenv("ZC_LZO_BATCH_BLOCKS");
+  const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
+  return v >= 1 && v < kMaxBatchBlocks ? (uint32_t)v : kMaxBatchBlocks;
+}
 
 }  // namespace
 
@@ -371,13 +379,14 @@ static hipError_t lzo_batch(LzoScratch* s, const uint8_t* d_payload, const uint6
 hipError_t lzo_compress(LzoScratch* s, const uint8_t* d_payload, const uint64_t* pay_off, const uint64_t* pay_size,
                         size_t n, uint8_t* d_out, const uint64_t* out_off, uint64_t* out_size, hipStream_t st) {
   s->times = LzoTimes{};
+  const uint32_t cap = max_batch_blocks();
   size_t b0 = 0;
   while (b0 < n) {
     size_t b1 = b0;
     uint64_t blk = 0;
     while (b1 < n) {
       const uint32_t k = zclzo::block_count(pay_size[b1]);
-      if (b1 > b0 && blk + k > kMaxBatchBlocks) break;
+      if (b1 > b0 && blk + k > cap) break;
       blk += k;
       b1++;
     }
