@@ -6,6 +6,8 @@ short pieces -- at random chunk sizes W in [64, 70000] besides the usual ones,
 device-resident; every fifth also seeded with the ids of another stream's
 chunks (ChunkIndex::loadIndex), every seventh fed through the host feed in
 ragged pieces through the smallest window."""
+import os
+
 import numpy as np
 import pytest
 
@@ -43,9 +45,11 @@ def _spec(rng, W):
     return ",".join(segs)
 
 
-@pytest.mark.parametrize("seed", range(400))
+# ZC_FUZZ_SEEDS / ZC_FUZZ_BASE widen or move the sweep (a longer run by hand)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZC_FUZZ_SEEDS", "400"))))
 def test_fuzz_vs_oracle(torch_cuda, seed):
     from zbackup_amd import BackupCreator
+    seed += int(os.environ.get("ZC_FUZZ_BASE", "0"))
     rng = np.random.default_rng(77000 + seed)
     W = int(rng.choice([64, 65, 127, 128, 255, 256, 999, 4095, 4096, 65536])) if seed % 2 else int(
         rng.integers(64, 70001))
