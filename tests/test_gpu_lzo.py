@@ -75,10 +75,14 @@ def test_lzo_edge_sizes_every_kind(torch_cuda, comp):
 
 
 def test_lzo_random_sizes(torch_cuda, comp):
-    rng = np.random.default_rng(2)
-    payloads = [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 3_000_000)), 200 + i) for i in range(48)]
-    got = _compress(torch_cuda, comp, payloads, rng)
-    _check(payloads, got)
+    # ZC_LZO_SWEEP=<rounds> repeats this with other seeds (a longer run by hand)
+    import os
+    for rnd in range(int(os.environ.get("ZC_LZO_SWEEP", "1"))):
+        rng = np.random.default_rng(2 + 1000 * rnd)
+        payloads = [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 3_000_000)), 200 + i + 100000 * rnd)
+                    for i in range(48)]
+        got = _compress(torch_cuda, comp, payloads, rng)
+        _check(payloads, got)
     for p, g in zip(payloads[:12], got):  # and the library decompresses them
         assert lzo_oracle.unframe(g) == p.tobytes()
 
