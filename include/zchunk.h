@@ -5,7 +5,10 @@
  * /root/reference/backup_creator.cc for the same bytes, chunk.max_size and
  * index contents.  Plain C types only; every call returns an int status
  * (ZC_OK == 0, negative on error; zc_last_error() has the message).  One
- * context per stream per GPU; a context is not shared between threads.
+ * context per stream per GPU.  Every entry point that takes a context holds a
+ * per-context lock for the whole call, so calls on one context from several
+ * threads are serialized; give each concurrent thread (a bundle compressor
+ * beside the feeding thread, say) a context of its own for concurrency.
  *
  * Reference interfaces each entry point replaces:
  *   zc_create              BackupCreator::BackupCreator(Config const &, ChunkIndex &,
@@ -144,7 +147,7 @@ int zc_chunk_device(zc_ctx* ctx, const void* d_data, uint64_t n);
  * backup_creator.cc's loop, with the feed's copies overlapped with the work */
 int zc_chunk_host(zc_ctx* ctx, const void* host, uint64_t n);
 
-size_t zc_record_count(const zc_ctx* ctx);  /* records held (cut and not yet taken) */
+size_t zc_record_count(const zc_ctx* ctx);  /* complete records held (cut, ids filled in, not yet taken) */
 int zc_get_records(const zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);
 /* move up to cap complete records out of the context, in stream order */
 int zc_take_records(zc_ctx* ctx, zc_record* out, size_t cap, size_t* n_out);

@@ -30,6 +30,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -190,12 +191,49 @@ public:
 ///
 /// (EncryptedFile::OutputStream::write, as bundle.cc:84 uses it), followed by the
 /// os.writeAdler32() the reference already does.
+///
+/// Bundle::Creator::write runs on detached compressor threads, several at a time
+/// (chunk_storage.cc:133-141,175), while the main thread feeds the backup stream
+/// through GpuChunkIndex's context.  So this class never touches that context:
+/// it keeps a pool of contexts of its own, one per compressor thread that is
+/// inside compress() at the moment (made on first need, reused after), and each
+/// call runs on a context no other thread is using.  (libzchunk also serializes
+/// the calls on one context with a per-context lock, so sharing one would be
+/// safe, only not concurrent.)
 class GpuLzoBundleCompressor: NoCopy
 {
-  zc_ctx * ctx;
+  int device;
+  std::mutex poolMutex;
+  std::vector< zc_ctx * > idle, all;
+
+  zc_ctx * acquire()
+  {
+    std::lock_guard< std::mutex > lock( poolMutex );
+    if ( !idle.empty() )
+    {
+      zc_ctx * c = idle.back();
+      idle.pop_back();
+      return c;
+    }
+    zc_ctx * c = 0;
+    zcCheck( zc_create( &c, 65536, device, 0 ), 0, "zc_create" );
+    all.push_back( c );
+    return c;
+  }
+
+  void release( zc_ctx * c )
+  {
+    std::lock_guard< std::mutex > lock( poolMutex );
+    idle.push_back( c );
+  }
 
 public:
-  explicit GpuLzoBundleCompressor( GpuChunkIndex & index ): ctx( index.context() ) {}
+  explicit GpuLzoBundleCompressor( int device_ = 0 ): device( device_ ) {}
+  ~GpuLzoBundleCompressor()
+  {
+    for ( size_t i = 0; i < all.size(); ++i )
+      zc_destroy( all[ i ] );
+  }
 
   void compress( string const & payload, string & framed )
   {
@@ -225,8 +263,13 @@ public:
     for ( size_t i = 0; i < n; ++i )
       in += *payloads[ i ];
     out.resize( outPos ? outPos : 1 );
-    zcCheck( zc_lzo_compress_host( ctx, in.data(), payOff.data(), paySize.data(), n, &out[ 0 ], outOff.data(),
-                                   outSize.data() ), ctx, "zc_lzo_compress_host" );
+    zc_ctx * ctx = acquire();
+    int rc = zc_lzo_compress_host( ctx, in.data(), payOff.data(), paySize.data(), n, &out[ 0 ], outOff.data(),
+                                   outSize.data() );
+    string err = rc == ZC_OK ? string() : string( zc_last_error( ctx ) );
+    release( ctx );
+    if ( rc != ZC_OK )
+      throw std::runtime_error( "zc_lzo_compress_host: " + err );
     framed.resize( n );
     for ( size_t i = 0; i < n; ++i )
       framed[ i ].assign( out, outOff[ i ], outSize[ i ] );

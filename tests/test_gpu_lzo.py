@@ -219,3 +219,59 @@ def test_lzo_call_split_into_batches(torch_cuda, comp, monkeypatch):
     rng = np.random.default_rng(9)
     payloads = [payload(KINDS[i % len(KINDS)], int(rng.integers(0, 400000)), 900 + i) for i in range(40)]
     _check(payloads, _compress(torch_cuda, comp, payloads, rng))
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_compressor_threads_beside_a_feed(torch_cuda, shared):
+    # Bundle::Creator::write runs on several compressor threads at once
+    # (chunk_storage.cc:133-141,175) while the main thread is inside
+    # handleMoreData.  Own contexts (shared=False, GpuLzoBundleCompressor's pool)
+    # run concurrently; one context shared by every thread (shared=True) is
+    # serialized by the per-context lock.  Every frame equals liblzo2's and the
+    # fed stream's records equal the oracle's.
+    import threading
+
+    from zbackup_amd import BackupCreator
+    from zbackup_amd.bundle import BundleCompressor
+    W = 4096
+    data = oracle.gen("R5:9000000,C100:3000000,Z:500000,R6:4000000")
+    want = oracle.chunk(data, W)
+    payloads = [[payload(k, int(s), 31 * t + i) for i, (k, s) in
+                 enumerate(zip(KINDS * 2, [2097152, 700001, 49173, 1234567, 98304, 2000000, 5, 333333, 49152,
+                                           1 << 20, 77777, 600000]))] for t in range(4)]
+    shared_comp = BundleCompressor() if shared else None
+    errors, results = [], [None] * 4
+
+    def compressor(t):
+        try:
+            comp = shared_comp or BundleCompressor()
+            out = []
+            for _ in range(3):
+                out = comp.compress_host([p.tobytes() for p in payloads[t]])
+            results[t] = out
+            if not shared:
+                comp.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=compressor, args=(t,)) for t in range(4)]
+    with BackupCreator(W, window=8 * W + (16 << 20)) as bc:
+        for th in threads:
+            th.start()
+        pos = 0
+        while pos < data.size:  # the main thread feeds meanwhile
+            buf = bc.get_input_buffer()
+            take = min(bc.get_input_buffer_size(), 1 << 20, data.size - pos)
+            np.frombuffer(buf, dtype=np.uint8, count=take)[:] = data[pos:pos + take]
+            bc.handle_more_data(take)
+            pos += take
+        bc.finish()
+        got = bc.record_tuples()
+        for th in threads:
+            th.join()
+    if shared_comp is not None:
+        shared_comp.close()
+    assert not errors, errors
+    assert got == want
+    for t in range(4):
+        _check(payloads[t], results[t])

@@ -371,3 +371,35 @@ def test_edited_duplicate_vs_oracle(torch_cuda, W, block, piece):
     assert sum(1 for r in want if r[0] == "D") > block // W // 2
     assert _run_device(torch_cuda, data, W) == want
     assert _run_host_feed(data, W) == want
+
+
+@pytest.mark.parametrize("sha1", [True, False])
+def test_backup_data_of_a_long_windowed_stream(torch_cuda, sha1):
+    # a stream many windows long whose first records are a bytes_to_emit
+    # fragment (50 bytes between a chunk and its copy) and a short chunk: the
+    # records are serialized as they are taken, while their bytes are still in
+    # the window; getBackupData at the end equals the oracle's stream
+    from zbackup_amd import BackupCreator, chunk_id_blob, serialize_instruction
+    W = 4096
+    data = oracle.gen("R1:4096,R2:50,C0:4096,R3:300,C4146:4096,R4:70000000,C0:4096")
+    want = oracle.chunk(data, W)
+    assert want[1][0] == "B" and want[1][2] == 50
+    expect = b""
+    for (k, off, size, h, sha) in want:
+        if k == "B":
+            expect += serialize_instruction(raw=data[off:off + size].tobytes())
+        else:
+            expect += serialize_instruction(chunk_blob=chunk_id_blob(bytes.fromhex(sha) if sha1 else bytes(16), h))
+    with BackupCreator(W, sha1=sha1, window=8 * W + (16 << 20)) as bc:
+        pos = 0
+        while pos < data.size:
+            buf = bc.get_input_buffer()
+            take = min(bc.get_input_buffer_size(), data.size - pos)
+            np.frombuffer(buf, dtype=np.uint8, count=take)[:] = data[pos:pos + take]
+            bc.handle_more_data(take)
+            pos += take
+        bc.finish()
+        assert bc.stats()["segments"] >= 3
+        assert bc.get_backup_data() == expect
+        if sha1:
+            assert bc.record_tuples() == want

@@ -71,7 +71,7 @@ class BackupCreator:
         if rc != _lib.ZC_OK:
             raise _lib.ZcError(f"zc_create failed ({rc})")
         self._ctx = ctx
-        self._data_taken = False
+        self._new_stream()
         if window is not None:
             _check(self._L, self._ctx, self._L.zc_set_window(self._ctx, int(window)), "zc_set_window")
         seeds = list(seeds)
@@ -82,6 +82,41 @@ class BackupCreator:
                 arr[i].rolling = rolling
                 arr[i].size = size
             _check(self._L, self._ctx, self._L.zc_seed_index(self._ctx, arr, len(seeds)), "zc_seed_index")
+
+    def _new_stream(self):
+        # A fed stream's records are taken from the context as they are cut and
+        # serialized right away, while their bytes are still in the feed window
+        # (bytes_to_emit reads them): BackupCreator::outputInstruction also runs
+        # inside handleMoreData (backup_creator.cc:267-273).  A long stream through
+        # a bounded window would otherwise have evicted them by getBackupData.
+        self._data = bytearray()  # BackupInstruction stream of the records taken
+        self._taken = []          # record arrays taken from the context, stream order
+        self._given = 0           # arrays of _taken that take_records() has returned
+        self._data_taken = False
+
+    def _drain(self):
+        """Take the complete records from the context and serialize them now."""
+        n = self._L.zc_record_count(self._ctx)
+        if not n:
+            return
+        out = np.zeros(n, dtype=RECORD_DTYPE)
+        got = ctypes.c_size_t()
+        _check(self._L, self._ctx,
+               self._L.zc_take_records(self._ctx, out.ctypes.data_as(ctypes.POINTER(_lib.ZcRecord)), n,
+                                       ctypes.byref(got)), "zc_take_records")
+        out = out[: got.value]
+        self._data += self._serialize(out)
+        self._taken.append(out)
+
+    def _serialize(self, recs):
+        recs = np.ascontiguousarray(recs)
+        need = ctypes.c_size_t()
+        self._L.zc_serialize_records(self._ctx, recs.ctypes.data, len(recs), None, 0, ctypes.byref(need))
+        out = np.zeros(max(need.value, 1), dtype=np.uint8)
+        rc = self._L.zc_serialize_records(self._ctx, recs.ctypes.data, len(recs), out.ctypes.data, out.size,
+                                          ctypes.byref(need))
+        _check(self._L, self._ctx, rc, "zc_serialize_records")
+        return out[:need.value].tobytes()
 
     # -- feed contract -------------------------------------------------------
     def get_input_buffer(self):
@@ -97,18 +132,22 @@ class BackupCreator:
 
     def handle_more_data(self, added):
         _check(self._L, self._ctx, self._L.zc_handle_more_data(self._ctx, added), "handleMoreData")
+        self._drain()
 
     def feed(self, data):
         data = np.ascontiguousarray(np.frombuffer(memoryview(data), dtype=np.uint8))
         _check(self._L, self._ctx, self._L.zc_feed(self._ctx, data.ctypes.data, data.size), "zc_feed")
+        self._drain()
 
     def finish(self):
         _check(self._L, self._ctx, self._L.zc_finish(self._ctx), "finish")
+        self._drain()
 
     # -- device-resident stream ----------------------------------------------
     def chunk_device(self, ptr, n):
         """Process `n` bytes already in HBM at device pointer `ptr` (e.g. a torch
         uint8 tensor's data_ptr()); feed + finish in one call."""
+        self._new_stream()
         _check(self._L, self._ctx, self._L.zc_chunk_device(self._ctx, ctypes.c_void_p(ptr), n),
                "zc_chunk_device")
 
@@ -116,10 +155,11 @@ class BackupCreator:
         """Process `n` bytes in host memory at address `ptr` (pinned for full
         speed): HBM copies in 64 MiB segments overlapped with the scan, then
         the same pipeline as chunk_device (zutils.cc:100-124 read loop + finish)."""
+        self._new_stream()
         _check(self._L, self._ctx, self._L.zc_chunk_host(self._ctx, ctypes.c_void_p(ptr), n), "zc_chunk_host")
 
     # -- results -------------------------------------------------------------
-    def records(self):
+    def _held(self):
         n = self._L.zc_record_count(self._ctx)
         out = np.zeros(n, dtype=RECORD_DTYPE)
         got = ctypes.c_size_t()
@@ -128,16 +168,21 @@ class BackupCreator:
                                       ctypes.byref(got)), "zc_get_records")
         return out[: got.value]
 
+    def records(self):
+        """Every record of the stream so far, in stream order (those already
+        taken from the context and those it still holds)."""
+        held = self._held()
+        if not self._taken:
+            return held
+        return np.concatenate(self._taken + [held])
+
     def take_records(self):
-        """Complete records cut so far, moved out of the context (the
+        """Complete records cut since the last take_records() (the
         instructions outputInstruction writes during handleMoreData)."""
-        n = self._L.zc_record_count(self._ctx)
-        out = np.zeros(n, dtype=RECORD_DTYPE)
-        got = ctypes.c_size_t()
-        _check(self._L, self._ctx,
-               self._L.zc_take_records(self._ctx, out.ctypes.data_as(ctypes.POINTER(_lib.ZcRecord)), n,
-                                       ctypes.byref(got)), "zc_take_records")
-        return out[: got.value]
+        self._drain()
+        new = self._taken[self._given:]
+        self._given = len(self._taken)
+        return np.concatenate(new) if new else np.zeros(0, dtype=RECORD_DTYPE)
 
     @property
     def window(self):
@@ -159,14 +204,8 @@ class BackupCreator:
         if self._data_taken:
             raise _lib.ZcError("getBackupData() called twice")
         self._data_taken = True
-        recs = np.ascontiguousarray(self.records())
-        need = ctypes.c_size_t()
-        self._L.zc_serialize_records(self._ctx, recs.ctypes.data, len(recs), None, 0, ctypes.byref(need))
-        out = np.zeros(max(need.value, 1), dtype=np.uint8)
-        rc = self._L.zc_serialize_records(self._ctx, recs.ctypes.data, len(recs), out.ctypes.data, out.size,
-                                          ctypes.byref(need))
-        _check(self._L, self._ctx, rc, "zc_serialize_records")
-        return out[:need.value].tobytes()
+        self._drain()
+        return bytes(self._data)
 
     def stats(self):
         st = _lib.ZcStats()
@@ -184,7 +223,7 @@ class BackupCreator:
 
     def reset(self):
         _check(self._L, self._ctx, self._L.zc_reset(self._ctx), "zc_reset")
-        self._data_taken = False
+        self._new_stream()
 
     def forget_stream_chunks(self):
         """Drop the index entries this context's streams added (Writer::add ->

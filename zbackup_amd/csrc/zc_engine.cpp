@@ -358,10 +358,16 @@ struct zc_ctx {
   DevBuf<uint32_t> hfilt;
   uint32_t hbits = 0;
 
-  // records: recs holds those not yet taken (zc_take_records); the first
-  // nrec_done of them are complete (digests and chunk ids filled in)
+  // records: recs[rec_head, nrec_done) are complete (digests and chunk ids
+  // filled in) and not yet taken (zc_take_records); records past nrec_done are
+  // being cut.  The taken prefix is dropped once it is most of the vector, so
+  // draining a long stream in small batches stays linear.
   std::vector<zc_record, DefaultInit<zc_record>> recs;  // resize leaves new records to be written
   size_t nrec_done = 0;
+  size_t rec_head = 0;
+  // every entry point holds this: calls on one context from several threads
+  // are serialized (a bundle compressor thread and the feeding thread, say)
+  mutable std::recursive_mutex mu;
   zc_stats stats{};
 
   LzoScratch* lzo = nullptr;  // bundle compression (zc_lzo.hip), made on first use
@@ -564,6 +570,7 @@ class Resolver {
     t_begin_ = Clock::now();
     c_.recs.clear();
     c_.nrec_done = 0;
+    c_.rec_head = 0;
     if (!windowed_) c_.recs.reserve(std::min<uint64_t>(n_ / W_ + 16, 1u << 24));
     c_.stats = zc_stats{};
     c_.stats.bytes = n_;
@@ -2125,6 +2132,11 @@ class Resolver {
   }
 };
 
+// every entry point on a context holds its mutex (null-safe)
+#define ZC_LOCK(c)                                                                                 \
+  std::unique_lock<std::recursive_mutex> zc_lk_ =                                                  \
+      (c) ? std::unique_lock<std::recursive_mutex>((c)->mu) : std::unique_lock<std::recursive_mutex>()
+
 int fail(zc_ctx* c, const ZcError& e) {
   if (c) c->err = e.msg;
   return e.code;
@@ -2333,6 +2345,7 @@ int zc_destroy(zc_ctx* c) {
 }
 
 int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
+  ZC_LOCK(c);
   if (!c || (n && !seeds)) return ZC_ERR_ARG;
   return guarded(c, [&] {
     for (size_t i = 0; i < n; ++i) {
@@ -2343,6 +2356,7 @@ int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
 }
 
 int zc_set_window(zc_ctx* c, uint64_t bytes) {
+  ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   if (c->res || c->n_stream) return ZC_ERR_STATE;
   c->win_cap = bytes ? window_for(bytes, c->W) : 0;
@@ -2352,6 +2366,7 @@ int zc_set_window(zc_ctx* c, uint64_t bytes) {
 uint64_t zc_get_window(const zc_ctx* c) { return c ? c->win_cap : 0; }
 
 void* zc_get_input_buffer(zc_ctx* c) {
+  ZC_LOCK(c);
   if (!c || c->finished) return nullptr;
   if (!c->win_cap) return c->stage;
   void* p = nullptr;
@@ -2365,6 +2380,7 @@ void* zc_get_input_buffer(zc_ctx* c) {
 }
 
 size_t zc_get_input_buffer_size(zc_ctx* c) {
+  ZC_LOCK(c);
   if (!c || c->finished) return 0;
   if (!c->win_cap) return kFeedChunk;
   size_t n = 0;
@@ -2378,6 +2394,7 @@ size_t zc_get_input_buffer_size(zc_ctx* c) {
 }
 
 int zc_handle_more_data(zc_ctx* c, size_t added) {
+  ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   if (c->finished) return ZC_ERR_STATE;
   if (!c->win_cap) {
@@ -2395,6 +2412,7 @@ int zc_handle_more_data(zc_ctx* c, size_t added) {
 }
 
 int zc_feed(zc_ctx* c, const void* host, size_t n) {
+  ZC_LOCK(c);
   if (!c || (n && !host)) return ZC_ERR_ARG;
   if (c->finished) return ZC_ERR_STATE;
   if (!c->win_cap) {
@@ -2419,6 +2437,7 @@ int zc_feed(zc_ctx* c, const void* host, size_t n) {
 }
 
 int zc_finish(zc_ctx* c) {
+  ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   if (c->finished) return ZC_ERR_STATE;
   if (c->win_cap) {
@@ -2449,6 +2468,7 @@ int zc_finish(zc_ctx* c) {
 }
 
 int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
+  ZC_LOCK(c);
   if (!c || (n && !d_data) || ((uintptr_t)d_data & 15)) return ZC_ERR_ARG;
   if (c->res) return ZC_ERR_STATE;  // a fed stream is open
   return guarded(c, [&] {
@@ -2467,6 +2487,7 @@ int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
 }
 
 int zc_chunk_host(zc_ctx* c, const void* host, uint64_t n) {
+  ZC_LOCK(c);
   if (!c || (n && !host)) return ZC_ERR_ARG;
   if (c->res) return ZC_ERR_STATE;
   return guarded(c, [&] {
@@ -2497,29 +2518,42 @@ int zc_chunk_host(zc_ctx* c, const void* host, uint64_t n) {
   });
 }
 
-size_t zc_record_count(const zc_ctx* c) { return c ? c->recs.size() : 0; }
+size_t zc_record_count(const zc_ctx* c) {
+  if (!c) return 0;
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
+  return c->nrec_done - c->rec_head;
+}
 
 int zc_get_records(const zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
   if (!c || (cap && !out)) return ZC_ERR_ARG;
-  size_t n = std::min(cap, c->recs.size());
-  if (n) memcpy(out, c->recs.data(), n * sizeof(zc_record));
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
+  size_t n = std::min(cap, c->nrec_done - c->rec_head);
+  if (n) memcpy(out, c->recs.data() + c->rec_head, n * sizeof(zc_record));
   if (n_out) *n_out = n;
   return ZC_OK;
 }
 
 int zc_take_records(zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
   if (!c || (cap && !out)) return ZC_ERR_ARG;
-  const size_t n = std::min(cap, c->nrec_done);
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
+  const size_t n = std::min(cap, c->nrec_done - c->rec_head);
   if (n) {
-    memcpy(out, c->recs.data(), n * sizeof(zc_record));
-    c->recs.erase(c->recs.begin(), c->recs.begin() + n);
-    c->nrec_done -= n;
+    memcpy(out, c->recs.data() + c->rec_head, n * sizeof(zc_record));
+    c->rec_head += n;
+    // between calls every record cut is complete (nrec_done == size): drop
+    // the taken prefix once it is most of the vector (amortised O(1) per record)
+    if (c->rec_head >= 65536 && 2 * c->rec_head >= c->recs.size() && c->nrec_done == c->recs.size()) {
+      c->recs.erase(c->recs.begin(), c->recs.begin() + c->rec_head);
+      c->nrec_done -= c->rec_head;
+      c->rec_head = 0;
+    }
   }
   if (n_out) *n_out = n;
   return ZC_OK;
 }
 
 int zc_get_stats(const zc_ctx* c, zc_stats* out) {
+  ZC_LOCK(c);
   if (!c || !out) return ZC_ERR_ARG;
   *out = c->stats;
   out->hbm_bytes = ctx_hbm_bytes(*c);
@@ -2529,6 +2563,7 @@ int zc_get_stats(const zc_ctx* c, zc_stats* out) {
 }
 
 int zc_reset(zc_ctx* c) {
+  ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   if (c->res) {
     (void)hipStreamSynchronize(c->stream);
@@ -2541,11 +2576,13 @@ int zc_reset(zc_ctx* c) {
   c->n_last = 0;
   c->recs.clear();
   c->nrec_done = 0;
+  c->rec_head = 0;
   c->err.clear();
   return ZC_OK;
 }
 
 int zc_forget_stream_chunks(zc_ctx* c) {
+  ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   return guarded(c, [&] {
     DeviceGuard g(c->device);
@@ -2557,6 +2594,7 @@ int zc_forget_stream_chunks(zc_ctx* c) {
 }
 
 int zc_read_stream(const zc_ctx* c, uint64_t offset, size_t n, void* host_out) {
+  ZC_LOCK(c);
   if (!c || (n && !host_out)) return ZC_ERR_ARG;
   if (c->windowed_last) {
     // the bytes still in the window (the host mirror)
@@ -2595,6 +2633,7 @@ static uint8_t* put_varint(uint8_t* p, uint64_t v) {
 }
 
 int zc_serialize_records(const zc_ctx* c, const zc_record* recs, size_t n, void* out, size_t cap, size_t* n_out) {
+  ZC_LOCK(c);
   if (!c || (n && !recs) || !n_out || (cap && !out)) return ZC_ERR_ARG;
   size_t need = 0;
   for (size_t i = 0; i < n; ++i) {
@@ -2672,6 +2711,7 @@ static int lzo_fail(zc_ctx* c, hipError_t e, const char* what) {
 
 int zc_bundle_gather(zc_ctx* c, const void* d_src, const uint64_t* src_off, const uint64_t* sizes, size_t n,
                      void* d_payload) {
+  ZC_LOCK(c);
   if (!c || (n && (!d_src || !src_off || !sizes || !d_payload))) return ZC_ERR_ARG;
   if (!n) return ZC_OK;
   DeviceGuard g(c->device);
@@ -2692,6 +2732,7 @@ uint64_t zc_lzo_capacity(uint64_t payload_size) { return payload_size + payload_
 
 int zc_lzo_compress(zc_ctx* c, const void* d_payload, const uint64_t* pay_off, const uint64_t* pay_size, size_t n,
                     void* d_out, const uint64_t* out_off, uint64_t* out_size) {
+  ZC_LOCK(c);
   if (!c || (n && (!d_payload || !pay_off || !pay_size || !d_out || !out_off || !out_size))) return ZC_ERR_ARG;
   for (size_t i = 0; i < n; i++)
     if (pay_size[i] > 0xffffffffull) {  // compression.cc:437-438
@@ -2716,6 +2757,7 @@ int zc_lzo_compress(zc_ctx* c, const void* d_payload, const uint64_t* pay_off, c
 
 int zc_lzo_compress_host(zc_ctx* c, const void* payload, const uint64_t* pay_off, const uint64_t* pay_size,
                          size_t n, void* out, const uint64_t* out_off, uint64_t* out_size) {
+  ZC_LOCK(c);
   if (!c || (n && (!payload || !pay_off || !pay_size || !out || !out_off || !out_size))) return ZC_ERR_ARG;
   uint64_t in_end = 0, out_end = 0;
   for (size_t i = 0; i < n; i++) {
@@ -2742,6 +2784,7 @@ int zc_lzo_compress_host(zc_ctx* c, const void* payload, const uint64_t* pay_off
 }
 
 int zc_adler32(zc_ctx* c, const void* d_base, const uint64_t* off, const uint64_t* len, size_t n, uint32_t* out) {
+  ZC_LOCK(c);
   if (!c || (n && (!d_base || !off || !len || !out))) return ZC_ERR_ARG;
   if (!n) return ZC_OK;
   DeviceGuard g(c->device);
@@ -2758,6 +2801,7 @@ int zc_adler32(zc_ctx* c, const void* d_base, const uint64_t* off, const uint64_
 }
 
 int zc_lzo_last_stats(const zc_ctx* c, double* parse_ms, uint64_t* blocks) {
+  ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   const LzoTimes t = c->lzo ? *lzo_times(c->lzo) : LzoTimes{};
   if (parse_ms) *parse_ms = t.parse_ms;
