@@ -58,9 +58,12 @@ class GpuChunkIndex: NoCopy, public IndexProcessor
   std::vector< zc_seed > seeds;
 
 public:
-  GpuChunkIndex( Config const & config, ChunkIndex & chunkIndex, int device ): ctx( 0 )
+  /// flags: ZC_FLAG_SHA1 (the default) is what zbackup needs -- the instruction
+  /// stream carries whole ChunkIds (backup_creator.cc:127-141,231-234)
+  GpuChunkIndex( Config const & config, ChunkIndex & chunkIndex, int device, uint32_t flags = ZC_FLAG_SHA1 ):
+    ctx( 0 )
   {
-    zcCheck( zc_create( &ctx, config.GET_STORABLE( chunk, max_size ), device, ZC_FLAG_SHA1 ), 0, "zc_create" );
+    zcCheck( zc_create( &ctx, config.GET_STORABLE( chunk, max_size ), device, flags ), 0, "zc_create" );
     chunkIndex.loadIndex( *this );  // every chunk id of every index file -> processChunk
     zcCheck( zc_seed_index( ctx, seeds.data(), seeds.size() ), ctx, "zc_seed_index" );
     std::vector< zc_seed >().swap( seeds );

@@ -1,0 +1,138 @@
+// BENCH TOOLING: the drop-in feed path end to end, in one process --
+// ZBackup::backupFromFileHandle's read loop (zutils.cc:100-127) over
+// integration/gpu_backup_creator.hh: the input copied into getInputBuffer()
+// (standing for fread, T copy threads), handleMoreData (the window's H2D
+// copies, scan and resolution during the call), the adapter draining the
+// records as they are cut (zc_take_records; a NEW chunk's bytes read with
+// zc_read_stream into Writer::add, which appends them to a 2 MiB bundle
+// payload; every record through Message::serialize), finish, getBackupData,
+// then the iterative shrink passes (zutils.cc:137-166) on the same index.
+//
+//   feed_bench W bytes seed sha1(0|1) copy_threads
+// prints one JSON object: seconds of the whole loop and of its parts
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gpu_backup_creator.hh"
+
+namespace {
+using Clock = std::chrono::steady_clock;
+double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
+// the engine's synthetic stream: byte k = byte k mod 8 of splitmix64 word k / 8
+void fill(uint8_t* p, uint64_t n, uint64_t seed, unsigned threads) {
+  std::vector<std::thread> th;
+  const uint64_t nw = n / 8;
+  for (unsigned t = 0; t < threads; ++t)
+    th.emplace_back([=] {
+      for (uint64_t i = nw * t / threads; i < nw * (t + 1) / threads; ++i) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        memcpy(p + 8 * i, &z, 8);
+      }
+    });
+  for (auto& x : th) x.join();
+  for (uint64_t k = nw * 8; k < n; ++k) p[k] = 0;
+}
+
+void copy_mt(void* dst, const void* src, size_t n, unsigned threads) {
+  if (threads <= 1 || n < (4u << 20)) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < threads; ++t) {
+    const size_t a = n * t / threads, b = n * (t + 1) / threads;
+    th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
+  }
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc != 6) {
+    fprintf(stderr, "usage: %s W bytes seed sha1 copy_threads\n", argv[0]);
+    return 2;
+  }
+  const uint32_t W = (uint32_t)strtoul(argv[1], 0, 10);
+  const uint64_t n = strtoull(argv[2], 0, 0), seed = strtoull(argv[3], 0, 0);
+  const bool sha1 = atoi(argv[4]) != 0;
+  const unsigned threads = (unsigned)atoi(argv[5]);
+  std::vector<uint8_t> input(n);
+  fill(input.data(), n, seed, 16);
+  StorableConfig st;
+  st.chunk_.max_size_ = W;
+  Config config;
+  config.storable = &st;
+  ChunkIndex chunkIndex;
+  ChunkStorage::Writer writer;
+  try {
+    GpuChunkIndex gpuIndex(config, chunkIndex, 0, sha1 ? ZC_FLAG_SHA1 : 0);
+    double copy_s = 0;
+    size_t pieces = 0;
+    const auto t0 = Clock::now();
+    GpuBackupCreator backupCreator(gpuIndex, writer);
+    uint64_t pos = 0;
+    for (;;) {
+      size_t toRead = backupCreator.getInputBufferSize();
+      void* inputBuffer = backupCreator.getInputBuffer();
+      const size_t rd = (size_t)std::min<uint64_t>(toRead, n - pos);
+      if (!rd) break;
+      const auto tc = Clock::now();
+      copy_mt(inputBuffer, input.data() + pos, rd, threads);
+      copy_s += since(tc);
+      pos += rd;
+      ++pieces;
+      backupCreator.handleMoreData((unsigned)rd);
+    }
+    backupCreator.finish();
+    std::string serialized;
+    backupCreator.getBackupData(serialized);
+    const double loop_s = since(t0);
+    const auto ts = Clock::now();
+    unsigned iterations = 0;
+    for (;;) {  // zutils.cc:137-166
+      GpuBackupCreator shrink(gpuIndex, writer);
+      const char* ptr = serialized.data();
+      size_t left = serialized.size();
+      while (left) {
+        size_t bufferSize = shrink.getInputBufferSize();
+        size_t toCopy = bufferSize > left ? left : bufferSize;
+        memcpy(shrink.getInputBuffer(), ptr, toCopy);
+        shrink.handleMoreData((unsigned)toCopy);
+        ptr += toCopy;
+        left -= toCopy;
+      }
+      shrink.finish();
+      std::string newGen;
+      shrink.getBackupData(newGen);
+      if (newGen.size() < serialized.size()) {
+        serialized.swap(newGen);
+        ++iterations;
+      } else {
+        break;
+      }
+    }
+    const double shrink_s = since(ts);
+    zc_stats stats;
+    zc_get_stats(gpuIndex.context(), &stats);
+    printf("{\"bytes\": %llu, \"W\": %u, \"sha1\": %d, \"copy_threads\": %u, \"pieces\": %zu, \"loop_s\": %.6f, "
+           "\"copy_s\": %.6f, \"writer_add_s\": %.6f, \"engine_and_adapter_s\": %.6f, \"shrink_s\": %.6f, "
+           "\"shrink_iterations\": %u, \"writer_chunks\": %zu, \"writer_bytes\": %zu, \"bundles\": %zu, "
+           "\"backup_data_bytes\": %zu, \"window_bytes\": %llu}\n",
+           (unsigned long long)n, W, sha1 ? 1 : 0, threads, pieces, loop_s, copy_s, writer.seconds,
+           loop_s - copy_s - writer.seconds, shrink_s, iterations, writer.chunks, writer.bytes, writer.bundles + 1,
+           serialized.size(), (unsigned long long)stats.window_bytes);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "feed_bench: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

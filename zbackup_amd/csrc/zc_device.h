@@ -165,8 +165,10 @@ struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
 // CNT_POOL: anchors found; CNT_OVERFLOW: wave-tiles over their pool share;
 // CNT_FOVF: screen-run buffer overflow flag; CNT_ANCLESS: class leaders
 // without an anchor; CNT_CLASS: refs that are not the leader of their class
+// CNT_PAIRS: equal-key pairs to byte-check; CNT_SPAIRS: pairs of grid chunks
+// whose SHA-1 the side stream computes (ZC_FLAG_SHA1), decided by SHA-1 prefix
 enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_ANCLESS = 5, CNT_CLASS = 6,
-       CNT_PAIRS = 7, CNT_LAST = 8 };
+       CNT_PAIRS = 7, CNT_SPAIRS = 8, CNT_LAST = 9 };
 
 // --- launchers (return hipError_t of the launch) ---------------------------
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
@@ -195,7 +197,11 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
 //   3. per ref: cls = the lowest ref with an equal key whose bytes are equal
 //      (else itself; counters[CNT_CLASS] += refs that are not leaders), and
 //      the class leaders without an anchor listed at ancless
-//      (counters[CNT_ANCLESS]).
+//      (counters[CNT_ANCLESS]).  With gsha (ZC_FLAG_SHA1: the grid chunks'
+//      SHA-1, 20 bytes per chunk [q W, (q + 1) W), q < n_gsha), pairs of
+//      two such grid chunks are not byte-checked: they are counted in
+//      counters[CNT_SPAIRS] and decided by launch_class_sha once the SHA-1
+//      has been computed.
 // Refs [0, nconf) must have start/key/cg/cfp/anc uploaded (vis = 0, dead = 0).
 // The class table has 2^cbits >= 2 nref slots, the anchor table 2^tbits
 // (2 << tbits words of tab; tab may be null when the stream has no anchors).
@@ -216,10 +222,17 @@ struct EpochIndex {
   uint32_t* ancless;
   unsigned long long* counters;
   uint2* pairs;  // scratch: nref {ref, leader} pairs for the byte check
+  const uint8_t* gsha;  // null: every pair by bytes
+  uint64_t n_gsha;
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
                               hipStream_t s);
+// the SHA-1 pairs of the last launch_epoch_index (counters[CNT_SPAIRS]): key +
+// SHA-1-prefix equality (ChunkIndex::findChunk's test, chunk_index.cc:119-143)
+// decides the class; gsha must be complete (ordered after the SHA-1 kernel)
+hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, uint32_t W, const EpochIndex& ix,
+                            uint32_t nref, hipStream_t s);
 uint32_t probe_filter_words();
 
 // key and first anchor of chunks [starts[i], starts[i] + W) (resident)

@@ -313,6 +313,7 @@ struct zc_ctx {
   hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
   hipStream_t sha_stream = nullptr;   // SHA-1 of the grid chunks, beside the scan (ZC_FLAG_SHA1)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
+  hipEvent_t ev_sha = nullptr;  // the grid chunks' SHA-1 (sha_stream) are complete
   std::string err;
 
   // host feed
@@ -646,8 +647,7 @@ class Resolver {
         scan_check();
       }
     }
-    finalize_records();
-    stream_end_index();
+    finalize_records(true);
     const double ms = ms_since(t0);
     c_.stats.total_ms += ms;
     // the resolver's work overlaps the scan's tail (nothing waits for the scan
@@ -706,8 +706,30 @@ class Resolver {
   // sha16: the chunks' SHA-1 prefixes when known (16 bytes each), else
   // computed here.
   void hist_add(const std::vector<uint64_t>& starts, const uint8_t* sha16) {
+    const HistPending hp = hist_add_meta(starts);
+    if (!hp.k) return;
+    std::vector<uint8_t> sha;
+    if (!sha16) {
+      std::vector<uint32_t> len(hp.k, W_);
+      const std::vector<uint8_t> sha20 = sha1s(starts, len);
+      sha.resize(16 * (size_t)hp.k);
+      for (uint32_t i = 0; i < hp.k; ++i) memcpy(&sha[16 * (size_t)i], &sha20[20 * (size_t)i], 16);
+      sha16 = sha.data();
+    }
+    hist_add_sha(hp, sha16);
+  }
+
+  // The part of hist_add that needs no SHA-1: the entries' key, first anchor,
+  // gear and fingerprint (device), their table insert, the keys on the host.
+  // hist_add_sha completes the entries once their SHA-1 prefixes are known.
+  struct HistPending {
+    uint32_t e0 = 0, k = 0;
+    std::vector<uint32_t> anc;
+  };
+  HistPending hist_add_meta(const std::vector<uint64_t>& starts) {
+    HistPending hp;
     const uint32_t k = (uint32_t)starts.size();
-    if (!k || !indexable_) return;
+    if (!k || !indexable_) return hp;
     const uint32_t e0 = c_.nhist;
     c_.va.ensure(k);
     c_.hanc.grow_keep(e0 + k, e0, c_.stream);
@@ -717,32 +739,26 @@ class Resolver {
     h2d(c_, c_.va.p, starts.data(), k);
     HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, k, W_, pow257(W_), c_.hm_key.p, c_.hanc.p + e0, c_.hg.p + e0,
                         c_.hfp.p + e0, c_.stream));
-    std::vector<uint8_t> sha20;
-    if (!sha16) {
-      std::vector<uint32_t> len(k, W_);
-      c_.vlen.ensure(k);
-      c_.sha_out.ensure((size_t)k * 20);
-      h2d(c_, c_.vlen.p, len.data(), k);
-      HCK(launch_sha1(d_, c_.va.p, c_.vlen.p, k, c_.sha_out.p, c_.stream));
-      sha20.resize((size_t)k * 20);
-      d2h(c_, sha20.data(), c_.sha_out.p, sha20.size());
-    }
     c_.hkey.resize((size_t)e0 + k);
-    std::vector<uint32_t> anc(k);
+    hp.anc.resize(k);
     d2h(c_, c_.hkey.data() + e0, c_.hm_key.p, k);
-    d2h(c_, anc.data(), c_.hanc.p + e0, k);
+    d2h(c_, hp.anc.data(), c_.hanc.p + e0, k);
     sync(c_);
-    c_.hsha.resize(16 * ((size_t)e0 + k));
-    uint8_t* hs = c_.hsha.data() + 16 * (size_t)e0;
-    if (sha16) {
-      memcpy(hs, sha16, 16 * (size_t)k);
-    } else {
-      for (uint32_t i = 0; i < k; ++i) memcpy(hs + 16 * (size_t)i, &sha20[20 * (size_t)i], 16);
-    }
-    for (uint32_t i = 0; i < k; ++i)
-      if (anc[i] == ZC_NO_ANCHOR) add_static_once(c_, c_.hkey[e0 + i], hs + 16 * (size_t)i, 0);
     c_.nhist = e0 + k;
     hist_table(c_, e0);
+    hp.e0 = e0;
+    hp.k = k;
+    return hp;
+  }
+  // sha16: the entries' SHA-1 prefixes, 16 bytes each; entries without an
+  // anchor also join the by-value set of the exact screen
+  void hist_add_sha(const HistPending& hp, const uint8_t* sha16) {
+    if (!hp.k) return;
+    c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
+    uint8_t* hs = c_.hsha.data() + 16 * (size_t)hp.e0;
+    memcpy(hs, sha16, 16 * (size_t)hp.k);
+    for (uint32_t i = 0; i < hp.k; ++i)
+      if (hp.anc[i] == ZC_NO_ANCHOR) add_static_once(c_, c_.hkey[hp.e0 + i], hs + 16 * (size_t)i, 0);
   }
 
  private:
@@ -1001,6 +1017,7 @@ class Resolver {
     const HistTab ht = hist_tab();
     if (nref_ || ht.tab) {
       auto tm = Clock::now();
+      EpochIndex ix{};
       const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
       uint32_t tbits = 10;  // sized for every ref having an anchor
       while ((1u << tbits) < 2u * nref_) ++tbits;
@@ -1035,10 +1052,11 @@ class Resolver {
         c_.ckeys.ensure(1u << tbits);
         c_.c_cls.ensure(nref_);
         c_.cpairs.ensure(nref_);
-        const EpochIndex ix{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
-                            c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
-                            c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
-                            c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p};
+        ix = EpochIndex{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
+                        c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
+                        c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
+                        c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
+                        pre_sha_n_ ? c_.gsha.p : nullptr, pre_sha_n_};
         HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
       } else {
         HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
@@ -1065,6 +1083,22 @@ class Resolver {
       if (scan_check()) {  // the pool changed under this epoch: queue it again
         c_.stats.epochs--;
         return true;
+      }
+      if (nref_ && c_.h_cnt[CNT_SPAIRS]) {
+        // ZC_FLAG_SHA1: equal-key grid chunks whose SHA-1 the side stream
+        // computes are decided by key + SHA-1 prefix, as ChunkIndex::findChunk
+        // decides (chunk_index.cc:119-143) -- no byte comparison -- once the
+        // SHA-1 kernel is done; the probe then runs again on the final classes
+        HCK(hipStreamWaitEvent(c_.stream, c_.ev_sha, 0));
+        HCK(launch_class_sha(c_.gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
+        if (anchors) {
+          HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
+          HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                           c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap,
+                           c_.counters.p, c_.stream));
+        }
+        d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
+        sync(c_);
       }
       ncand = anchors ? c_.h_cnt[CNT_CAND] : 0;
       nancless = nref_ ? c_.h_cnt[CNT_ANCLESS] : 0;
@@ -2035,6 +2069,7 @@ class Resolver {
     c_.gsha.ensure(k * 20);
     HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
     HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+    HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
     pre_sha_n_ = k;
   }
 
@@ -2043,7 +2078,10 @@ class Resolver {
   // and (ZC_FLAG_SHA1) every chunk record its SHA-1 prefix.
   std::vector<uint64_t> fresh_;  // NEW W-byte chunks of the stream still resident: offset,
   std::vector<uint8_t> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
-  void finalize_records() {
+  // stream_end: the stream's end (run_final): with ZC_FLAG_SHA1 its new W-byte
+  // chunks join the context's index here, their device metadata queued before
+  // the wait for the grid SHA-1, so that wait ends the call with little after it
+  void finalize_records(bool stream_end = false) {
     auto t0 = Clock::now();
     struct Done {
       zc_stats& st;
@@ -2067,42 +2105,60 @@ class Resolver {
     std::vector<uint64_t> h = range_digests(a, b);
     for (size_t j = 0; j < rest.size(); ++j) c_.recs[need_digest_[rest[j]].rec].rolling = h[j];
     need_digest_.clear();
-    const size_t r0 = c_.nrec_done;
-    if (c_.flags & ZC_FLAG_SHA1) {
-      const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;
-      std::vector<uint64_t> sa;
-      std::vector<uint32_t> sl;
-      std::vector<size_t> idx;
-      const bool pow2 = (W_ & (W_ - 1)) == 0;
-      const int wsh = pow2 ? __builtin_ctzll(W_) : 0;
-      for (size_t i = r0; i < c_.recs.size(); ++i) {
+    const size_t r0 = c_.nrec_done, r1 = c_.recs.size();
+    const bool sha1 = c_.flags & ZC_FLAG_SHA1;
+    if (!sha1) {
+      c_.nrec_done = r1;
+      if (stream_end) stream_end_index(nullptr);
+      return;
+    }
+    // records that are a whole grid chunk take their SHA-1 from the side
+    // stream's pass; the others are hashed now
+    const bool pow2 = (W_ & (W_ - 1)) == 0;
+    const int wsh = pow2 ? __builtin_ctzll(W_) : 0;
+    auto grid_q = [&](const zc_record& r) -> uint64_t {  // grid chunk of the record, or kInf
+      const uint64_t q = pow2 ? r.offset >> wsh : r.offset / W_;
+      return q * W_ == r.offset && q < pre_sha_n_ && r.size == std::min<uint64_t>(W_, n_ - r.offset) ? q : kInf;
+    };
+    std::vector<uint64_t> sa;
+    std::vector<uint32_t> sl;
+    std::vector<size_t> idx;
+    const size_t f0 = fresh_.size();
+    for (size_t i = r0; i < r1; ++i) {
+      const zc_record& r = c_.recs[i];
+      if (r.kind == ZC_BYTES) continue;
+      if (r.kind == ZC_CHUNK_NEW && r.size == W_) fresh_.push_back(r.offset);
+      if (grid_q(r) != kInf) continue;
+      sa.push_back(r.offset);
+      sl.push_back(r.size);
+      idx.push_back(i);
+    }
+    std::vector<uint8_t> sh = sha1s(sa, sl);
+    HistPending hp;
+    if (stream_end) hp = hist_add_meta(fresh_);
+    const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;  // waits for the side stream
+    auto fill = [&](size_t a0, size_t a1) {
+      for (size_t i = r0 + a0; i < r0 + a1; ++i) {
         zc_record& r = c_.recs[i];
         if (r.kind == ZC_BYTES) continue;
-        const uint64_t q = pow2 ? r.offset >> wsh : r.offset / W_;
-        if (q * W_ == r.offset && q < pre_sha_n_ && r.size == std::min<uint64_t>(W_, n_ - r.offset)) {
-          memcpy(r.sha1, &gsha[q * 20], 16);
-          continue;
-        }
-        sa.push_back(r.offset);
-        sl.push_back(r.size);
-        idx.push_back(i);
+        const uint64_t q = grid_q(r);
+        if (q != kInf) memcpy(r.sha1, &gsha[q * 20], 16);
       }
-      for (size_t off = 0; off < sa.size(); off += kFBatchMax) {
-        size_t m = std::min(sa.size() - off, kFBatchMax);
-        std::vector<uint64_t> pa(sa.begin() + off, sa.begin() + off + m);
-        std::vector<uint32_t> pl(sl.begin() + off, sl.begin() + off + m);
-        std::vector<uint8_t> sh = sha1s(pa, pl);
-        for (size_t j = 0; j < m; ++j) memcpy(c_.recs[idx[off + j]].sha1, &sh[j * 20], 16);
-      }
-      for (size_t i = r0; i < c_.recs.size(); ++i) {
+    };
+    if (r1 - r0 >= kParallelRecordsMin) HostPool::get().run(r1 - r0, fill);
+    else fill(0, r1 - r0);
+    for (size_t j = 0; j < idx.size(); ++j) memcpy(c_.recs[idx[j]].sha1, &sh[j * 20], 16);
+    // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_
+    fresh_sha_.resize(16 * fresh_.size());
+    {
+      size_t f = f0;
+      for (size_t i = r0; i < r1 && f < fresh_.size(); ++i) {
         const zc_record& r = c_.recs[i];
-        if (r.kind == ZC_CHUNK_NEW && r.size == W_) {
-          fresh_.push_back(r.offset);
-          fresh_sha_.insert(fresh_sha_.end(), r.sha1, r.sha1 + 16);
-        }
+        if (r.kind == ZC_CHUNK_NEW && r.size == W_) memcpy(&fresh_sha_[16 * f++], r.sha1, 16);
       }
     }
-    c_.nrec_done = c_.recs.size();
+    c_.nrec_done = r1;
+    if (stream_end) stream_end_index(&hp);
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
@@ -2111,9 +2167,9 @@ class Resolver {
   // matches a committed one's index (chunk_index.cc:26-79).  Without it the
   // index is left as the stream found it (entries evicted from the window
   // during the stream are dropped again).
-  void stream_end_index() {
+  void stream_end_index(const HistPending* hp) {
     if (c_.flags & ZC_FLAG_SHA1) {
-      hist_add(fresh_, fresh_sha_.data());
+      hist_add_sha(*hp, fresh_sha_.data());
     } else {
       index_truncate(c_, hist0_, statics0_);
     }
@@ -2307,6 +2363,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreate(&c->ev_meta));
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_sha, hipEventDisableTiming));
     HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
@@ -2332,6 +2389,7 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_meta) (void)hipEventDestroy(c->ev_meta);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
+    if (c->ev_sha) (void)hipEventDestroy(c->ev_sha);
     if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);

@@ -675,13 +675,18 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
 // bytes before each half of a lane span (they prime the gear) are two
 // per-lane register loads issued together with the DMA of the half's first
 // round, so half and tile boundaries cost no extra pipeline round.
+struct ScanLds {
+  uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
+  uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
+  uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 3];
+};
 template <int ABL>
-__global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
+__device__ __forceinline__ void scan_body(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
-    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
-  __shared__ __attribute__((aligned(16))) uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
-  __shared__ uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 3];
-  __shared__ uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L) {
+  auto& ring = L.ring;
+  auto& wlist = L.wlist;
+  auto& wdata = L.wdata;
   constexpr uint32_t kRpt = kRounds;  // rounds per tile
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t grid = gridDim.x;
@@ -798,6 +803,25 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   }
 }
 
+template <int ABL>
+__global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
+  __shared__ ScanLds lds;
+  scan_body<ABL>(data, n, tile0, ntiles, lo_thr, blk, po, counters, lds);
+}
+// The same with at most 128 VGPRs, so two waves of another kernel (the grid
+// SHA-1 beside the scan) fit on each SIMD next to the scan's two.  The LDS is
+// dynamic (sizeof(ScanLds) at launch): with a static 160 KiB the compiler
+// derives two waves per SIMD from it and ignores the register bound.
+template <int ABL>
+__global__ void __launch_bounds__(ZC_SCAN_TPB, 2) zc_scan_kernel_v128(
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t zc_dyn_lds[];
+  scan_body<ABL>(data, n, tile0, ntiles, lo_thr, blk, po, counters, *(ScanLds*)zc_dyn_lds);
+}
+
 // the stream's last, partial tile: one 256-thread block per wave-tile, a
 // 1 KiB sub-span per thread (block digests and anchors)
 __global__ void __launch_bounds__(ZC_WT_BLOCK) zc_scan_tail_kernel(const uint8_t* __restrict__ data, uint64_t n,
@@ -863,6 +887,22 @@ __device__ __forceinline__ TileAnchors tile_anchors(const AnchorView& av, uint64
 
 // ---------------------------------------------------------------------------
 // the epoch's tables and counters, cleared by the chunk-metadata launch
+// The grid chunks' SHA-1 (zc_sha1_grid_kernel: 20 bytes per chunk [q W, (q + 1) W)
+// of the stream, q < n_sha), when the side stream computes them (ZC_FLAG_SHA1)
+struct ShaGrid {
+  const uint8_t* sha;  // null: none
+  uint64_t n_sha;
+  uint64_t n;
+  uint32_t W;
+  __device__ __forceinline__ bool has(uint64_t c) const {
+    return sha && c % W == 0 && c / W < n_sha && c + W <= n;
+  }
+  __device__ __forceinline__ uint4 prefix(uint64_t c) const {
+    const uint32_t* p = (const uint32_t*)(sha + c / W * 20);  // 4-byte aligned
+    return make_uint4(p[0], p[1], p[2], p[3]);
+  }
+};
+
 struct EpochClear {
   uint64_t* ckeys;  // class table {key high word | lowest ref}: empty
   uint32_t cwords;
@@ -1341,7 +1381,7 @@ __global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint
 __global__ void __launch_bounds__(256) zc_class_lead_kernel(
     const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off, uint32_t nref,
     const uint64_t* __restrict__ ckeys, uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
-    uint2* __restrict__ pairs, unsigned long long* __restrict__ counters) {
+    uint2* __restrict__ pairs, unsigned long long* __restrict__ counters, ShaGrid sg, const uint64_t* __restrict__ start) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nref) return;
   const uint64_t k = key[i];
@@ -1356,9 +1396,37 @@ __global__ void __launch_bounds__(256) zc_class_lead_kernel(
   cls[i] = i;
   if (lead == i) {
     if (anc_off[i] == ZC_NO_ANCHOR) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = i;
+  } else if (sg.has(start[i]) && sg.has(start[lead])) {
+    // both are grid chunks whose SHA-1 the side stream computes: the pair is
+    // decided by key + SHA-1 prefix (zc_class_sha_kernel), listed from the top
+    pairs[nref - 1 - atomicAdd(&counters[CNT_SPAIRS], 1ull)] = make_uint2(i, lead);
   } else {
     pairs[atomicAdd(&counters[CNT_PAIRS], 1ull)] = make_uint2(i, lead);
   }
+}
+
+// ZC_FLAG_SHA1: the pairs of grid chunks, thread per pair, by the 16-byte
+// SHA-1 prefix (their 64-bit keys are equal already): key + prefix equality is
+// ChunkIndex::findChunk's own test (chunk_index.cc:119-143), so no bytes are
+// read.  Equal -> cls = leader; else a ref without an anchor goes to the screen.
+__global__ void __launch_bounds__(256) zc_class_sha_kernel(ShaGrid sg, const uint64_t* __restrict__ start,
+                                                           const uint32_t* __restrict__ anc_off, uint32_t nref,
+                                                           uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
+                                                           const uint2* __restrict__ pairs,
+                                                           unsigned long long* __restrict__ counters) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = t < counters[CNT_SPAIRS];
+  bool same = false;
+  uint2 pr = make_uint2(0, 0);
+  if (live) {
+    pr = pairs[nref - 1 - t];
+    const uint4 a = sg.prefix(start[pr.x]), b = sg.prefix(start[pr.y]);
+    same = a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+    if (same) cls[pr.x] = pr.y;
+    else if (anc_off[pr.x] == ZC_NO_ANCHOR) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = pr.x;
+  }
+  const uint64_t joined = __popcll(__ballot(same));  // one counter atomic per wave
+  if ((threadIdx.x & 63) == 0 && joined) atomicAdd(&counters[CNT_CLASS], (unsigned long long)joined);
 }
 
 __global__ void __launch_bounds__(256) zc_class_verify_kernel(
@@ -2396,11 +2464,20 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
   hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
                      ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
   hipLaunchKernelGGL(zc_class_lead_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, nref,
-                     ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.pairs, ix.counters);
+                     ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.pairs, ix.counters,
+                     ShaGrid{ix.gsha, ix.gsha ? ix.n_gsha : 0, n, W}, ix.start);
   // persistent: up to 16 waves per CU (the pair count is on the device)
   const unsigned vblocks = (unsigned)std::min<uint64_t>(blocks_for(nref, 4), (uint64_t)cu_count() * 4);
   hipLaunchKernelGGL(zc_class_verify_kernel, dim3(vblocks), dim3(256), 0, s, data, ix.start, ix.anc, W, ix.cls,
                      ix.ancless, ix.pairs, ix.counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, uint32_t W, const EpochIndex& ix,
+                            uint32_t nref, hipStream_t s) {
+  if (!nref || !gsha) return hipSuccess;
+  hipLaunchKernelGGL(zc_class_sha_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ShaGrid{gsha, n_gsha, n, W},
+                     ix.start, ix.anc, nref, ix.cls, ix.ancless, ix.pairs, ix.counters);
   return hipGetLastError();
 }
 
