@@ -334,6 +334,40 @@ def bundle_leg(torch, buf, n, recs, world, local, cpu_sample):
     return res
 
 
+def stage_dict(st):
+    return {"scan_ms": round(st["scan_ms"], 4), "resolve_ms": round(st["resolve_ms"], 4),
+            "total_ms": round(st["total_ms"], 4), "anchors": st["anchors"],
+            "candidates": st["candidates"], "epochs": st["epochs"],
+            "meta_ms": round(st["meta_ms"], 4), "probe_ms": round(st["probe_ms"], 4),
+            "fscan_ms": round(st["fscan_ms"], 4), "walk_ms": round(st["walk_ms"], 4),
+            "finalize_ms": round(st["finalize_ms"], 4), "fbatch_ms": round(st["fbatch_ms"], 4)}
+
+
+def feed_bench(n, seed, sha1, copy_threads=8):
+    """tools/feedbench/feed_bench (built in-tree by build()): the zutils.cc read
+    loop over the C++ binding, one process; the input copy is split over
+    copy_threads threads and reported apart from the engine's time."""
+    exe = os.path.join(ROOT, "tools", "feedbench", "feed_bench")
+    if not os.path.exists(exe):
+        return None
+    out = subprocess.run([exe, str(W64), str(n), str(seed), "1" if sha1 else "0", str(copy_threads)],
+                         capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return {"error": out.stderr.strip()[-300:]}
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    eng = d["engine_and_adapter_s"]
+    return {"value": round(n / d["loop_s"] / 2**30, 3), "unit": "GiB/s",
+            "engine_and_adapter_GiB_per_s": round(n / eng / 2**30, 3) if eng > 0 else None,
+            "loop_s": d["loop_s"], "copy_s": d["copy_s"], "copy_threads": d["copy_threads"],
+            "writer_add_s": d["writer_add_s"], "engine_and_adapter_s": eng, "shrink_s": d["shrink_s"],
+            "shrink_iterations": d["shrink_iterations"], "writer_chunks": d["writer_chunks"],
+            "bundles": d["bundles"], "window_bytes": d["window_bytes"], "pieces": d["pieces"],
+            "path": "zutils.cc read loop over integration/gpu_backup_creator.hh: memcpy into getInputBuffer "
+                    f"({copy_threads} threads, standing for fread), handleMoreData through the bounded window, "
+                    "records drained as cut (zc_take_records, zc_read_stream -> Writer::add into 2 MiB bundle "
+                    "payloads, Message::serialize), finish, getBackupData; shrink passes timed apart"}
+
+
 def rank_env(args):
     """(world, rank, local rank) from the environment; joins the gloo group
     the replicas use for their barriers and max/gather reductions."""
@@ -430,13 +464,32 @@ def run_rank(args):
     # to the headline, the per-GPU fractions and the concurrent CPU baseline, so
     # N ranks do not each pin 8 GiB of host memory for the end-to-end legs
     if not args.no_extras and world == 1:
-        # complete ChunkIds on every record, same streams
+        # complete ChunkIds on every record (the mode the zbackup binding runs,
+        # integration/gpu_backup_creator.hh): C2, and C3 / C5 in a second buffer
         if not args.sha1 and args.sha1_steps > 0:
             b2 = BackupCreator(W64, device=local, sha1=True, timing=True)
             el2, _ = timed_steps(torch, world, make_step(b2, True), 2, args.sha1_steps)
-            b2.close()
+            st2 = b2.stats()
             extras["value_sha1"] = job_value(n, world, args.sha1_steps, el2)
             extras["sha1_ms_per_step"] = el2 / args.sha1_steps * 1e3
+            extras["sha1_stages"] = stage_dict(st2)
+            if args.config == "c2":
+                other = torch.empty(n, dtype=torch.uint8, device=buf.device)
+                for cfg in ("c3", "c5"):
+                    fill_stream(torch, other, n, cfg, seed, local)
+
+                    def step_other():
+                        b2.forget_stream_chunks()
+                        b2.chunk_device(other.data_ptr(), n)
+                        return 0.0
+
+                    elc, _ = timed_steps(torch, world, step_other, 2, args.sha1_steps)
+                    extras[f"value_sha1_{cfg}"] = {"value": round(job_value(n, world, args.sha1_steps, elc), 3),
+                                                   "unit": "GiB/s",
+                                                   "ms_per_step": round(elc / args.sha1_steps * 1e3, 3),
+                                                   "workload": CONFIGS[cfg], "stages": stage_dict(b2.stats())}
+                del other
+            b2.close()
         # incremental backups on one context: with SHA-1 ids a stream's chunks
         # stay in the context's index (Writer::add -> ChunkIndex::addChunk), so
         # a later stream is matched against them through the historic index --
@@ -465,62 +518,46 @@ def run_rank(args):
                               "new_records": int((kinds == 0).sum()), "hist_entries": st5["hist_entries"]}
             del other
             extras["incremental"] = inc
-        # the stream starts in (pinned) host memory, as in zutils.cc:100-124
+        # the stream starts in (pinned) host memory, as in zutils.cc:100-124:
+        # rolling-hash ids and complete ChunkIds
         host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
         host.copy_(buf)
-        b3 = BackupCreator(W64, device=local, sha1=False, timing=True)
         reps = 3
+        for sha1 in (False, True):
+            b3 = BackupCreator(W64, device=local, sha1=sha1, timing=True)
 
-        def e2e_step():
-            b3.chunk_host(host.data_ptr(), n)
-            return 0.0
+            def e2e_step():
+                if sha1:
+                    b3.forget_stream_chunks()
+                b3.chunk_host(host.data_ptr(), n)
+                return 0.0
 
-        el3, _ = timed_steps(torch, world, e2e_step, 1, reps)
-        e2e = job_value(n, world, reps, el3)
+            el3, _ = timed_steps(torch, world, e2e_step, 1, reps)
+            b3.close()
+            extras["end_to_end_sha1" if sha1 else "end_to_end"] = {
+                "value": job_value(n, world, reps, el3), "unit": "GiB/s", "ms_per_step": el3 / reps * 1e3,
+                "path": "pinned host buffer -> zc_chunk_host: 64 MiB H2D segments on a side stream, each scanned "
+                        "as it lands, then resolve + records to host" + (" + SHA-1 chunk ids" if sha1 else "")}
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(reps):
             buf.copy_(host, non_blocking=True)
         torch.cuda.synchronize()
         h2d = job_gather(n * reps / (time.perf_counter() - t1) / 2**30, world)
-        b3.close()
-        extras["end_to_end"] = {"value": e2e, "unit": "GiB/s", "ms_per_step": el3 / reps * 1e3,
-                                "path": "pinned host buffer -> zc_chunk_host: 64 MiB H2D segments on a side "
-                                        "stream, each scanned as it lands, then resolve + records to host",
-                                "h2d_only_GiB_per_s_per_gpu": [round(v, 2) for v in h2d]}
-        # the drop-in feed (zutils.cc:100-124): the stream is written into
-        # getInputBuffer() piece by piece (here a memcpy stands for fread) and
-        # chunked through the bounded window during handleMoreData, records
-        # drained as they are cut
-        import ctypes
-        src = host.data_ptr()
-        b4 = BackupCreator(W64, device=local, sha1=False, timing=True)
-        t1 = time.perf_counter()
-        nrec_feed = 0
-        pos = 0
-        copy_s = 0.0
-        while pos < n:
-            dst = b4._L.zc_get_input_buffer(b4._ctx)
-            room = b4.get_input_buffer_size()
-            m = min(room, n - pos)
-            tc = time.perf_counter()
-            ctypes.memmove(dst, src + pos, m)
-            copy_s += time.perf_counter() - tc
-            b4.handle_more_data(m)
-            pos += m
-            nrec_feed += len(b4.take_records())
-        b4.finish()
-        nrec_feed += len(b4.take_records())
-        feed_s = time.perf_counter() - t1
-        fst = b4.stats()
-        b4.close()
-        extras["feed"] = {"value": job_value(n, world, 1, job_max(feed_s, world)), "unit": "GiB/s",
-                          "path": "getInputBuffer/handleMoreData through the default bounded window "
-                                  f"({fst['window_bytes'] >> 20} MiB), a host memcpy per piece standing for "
-                                  "fread, records taken as they are cut",
-                          "records": nrec_feed, "segments": fst["segments"], "hbm_bytes": fst["hbm_bytes"],
-                          "host_memcpy_s": round(copy_s, 4), "feed_s": round(feed_s, 4)}
+        extras["end_to_end"]["h2d_only_GiB_per_s_per_gpu"] = [round(v, 2) for v in h2d]
+        fill_stream(torch, buf, n, args.config, seed, local)  # buf held the host copy's bytes anyway
         del host
+        # the drop-in feed (zutils.cc:100-127 over integration/gpu_backup_creator.hh,
+        # tools/feedbench): input copied into getInputBuffer() (standing for fread),
+        # handleMoreData through the bounded window, the adapter taking the records
+        # as they are cut (Writer::add of each new chunk's bytes into a 2 MiB bundle
+        # payload, Message::serialize of every record), finish, getBackupData, the
+        # shrink passes; rolling-hash ids and complete ChunkIds
+        if args.config == "c2":
+            for sha1 in (False, True):
+                fb = feed_bench(n, seed, sha1)
+                if fb:
+                    extras["feed_sha1" if sha1 else "feed"] = fb
         if args.config == "c2" and args.lzo:
             extras["bundle_lzo"] = bundle_leg(torch, buf, n, recs, world, local, rank == 0)
 
@@ -565,12 +602,7 @@ def run_rank(args):
                          "traffic": pmc_traffic(n), "bytes_per_launch": n,
                          "scan_ms_avg": round(scan_avg, 4)},
             "per_gpu_frac": [round(f, 4) for f in fracs],
-            "stages": {"scan_ms": round(st["scan_ms"], 4), "resolve_ms": round(st["resolve_ms"], 4),
-                       "total_ms": round(st["total_ms"], 4), "anchors": st["anchors"],
-                       "candidates": st["candidates"], "epochs": st["epochs"],
-                       "meta_ms": round(st["meta_ms"], 4), "probe_ms": round(st["probe_ms"], 4),
-                       "fscan_ms": round(st["fscan_ms"], 4), "walk_ms": round(st["walk_ms"], 4),
-                       "finalize_ms": round(st["finalize_ms"], 4), "fbatch_ms": round(st["fbatch_ms"], 4)},
+            "stages": stage_dict(st),
         }
         if rp_ms and args.config == "c2" and n == 8 << 30:
             # the same kernel's average under rocprofv3 (committed summary)
@@ -581,17 +613,21 @@ def run_rank(args):
         if "value_sha1" in extras:
             out["value_sha1"] = round(extras["value_sha1"], 3)
             out["sha1_ms_per_step"] = round(extras["sha1_ms_per_step"], 3)
-        if "end_to_end" in extras:
-            e = extras["end_to_end"]
-            e["value"] = round(e["value"], 3)
-            e["ms_per_step"] = round(e["ms_per_step"], 3)
-            out["end_to_end"] = e
+            out["sha1_stages"] = extras["sha1_stages"]
+        for key in ("value_sha1_c3", "value_sha1_c5"):
+            if key in extras:
+                out[key] = extras[key]
+        for key in ("end_to_end", "end_to_end_sha1"):
+            if key in extras:
+                e = extras[key]
+                e["value"] = round(e["value"], 3)
+                e["ms_per_step"] = round(e["ms_per_step"], 3)
+                out[key] = e
         if "incremental" in extras:
             out["incremental_sha1"] = extras["incremental"]
-        if "feed" in extras:
-            f = extras["feed"]
-            f["value"] = round(f["value"], 3)
-            out["feed"] = f
+        for key in ("feed", "feed_sha1"):
+            if key in extras:
+                out[key] = extras[key]
         if "bundle_lzo" in extras:
             out["bundle_lzo"] = extras["bundle_lzo"]
         if cpu:

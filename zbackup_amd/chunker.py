@@ -74,6 +74,11 @@ class BackupCreator:
         self._new_stream()
         if window is not None:
             _check(self._L, self._ctx, self._L.zc_set_window(self._ctx, int(window)), "zc_set_window")
+        self.seed_index(seeds)
+
+    def seed_index(self, seeds):
+        """Add (sha1_16, rolling, size) ids to the context's index (zc_seed_index:
+        what ChunkIndex::loadIndex registers, chunk_index.cc:26-79,163-182)."""
         seeds = list(seeds)
         if seeds:
             arr = (_lib.ZcSeed * len(seeds))()
