@@ -164,6 +164,11 @@ int zc_forget_stream_chunks(zc_ctx* ctx);
  * (the payload of BYTES records, for serializing bytes_to_emit, and of NEW
  * chunks, for Writer::add); for a fed stream, the bytes still in its window */
 int zc_read_stream(const zc_ctx* ctx, uint64_t offset, size_t n, void* host_out);
+/* the same bytes without a copy, for a fed stream: a pointer into the feed
+ * window's pinned host mirror, valid until the next zc_get_input_buffer /
+ * zc_get_input_buffer_size / zc_feed / zc_finish / zc_reset call; NULL when
+ * the range is not in host memory (a device-resident stream: zc_read_stream) */
+const void* zc_stream_data(const zc_ctx* ctx, uint64_t offset, size_t n);
 /* the records' BackupInstruction stream, as BackupCreator::outputInstruction writes it
  * (Message::serialize, message.cc:16-23: varint32 length + field 1 chunk_to_emit =
  * ChunkId::toBlob (chunk_id.cc:19-27) | field 2 bytes_to_emit, the record's bytes read from

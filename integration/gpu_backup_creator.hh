@@ -113,9 +113,16 @@ class GpuBackupCreator: NoCopy
       id.rollingHash = r.rolling;
       if ( r.kind == ZC_CHUNK_NEW )  // saveChunkToSave: backup_creator.cc:124-139
       {
-        bytes.resize( r.size );
-        zcCheck( zc_read_stream( ctx, r.offset, r.size, &bytes[ 0 ] ), ctx, "zc_read_stream" );
-        chunkStorageWriter.add( id, bytes.data(), r.size );
+        // the chunk's bytes straight from the feed window's host mirror (no
+        // copy); a device-resident stream's are copied out
+        void const * data = zc_stream_data( ctx, r.offset, r.size );
+        if ( !data )
+        {
+          bytes.resize( r.size );
+          zcCheck( zc_read_stream( ctx, r.offset, r.size, &bytes[ 0 ] ), ctx, "zc_read_stream" );
+          data = bytes.data();
+        }
+        chunkStorageWriter.add( id, data, r.size );
       }
       instr.set_chunk_to_emit( id.toBlob() );
     }

@@ -100,9 +100,9 @@ def test_static_key_with_wrong_prefix_is_no_match(torch_cuda, W, path):
     # an index entry whose key equals a real window's rolling hash, with another
     # SHA-1 prefix: findChunk finds the key, compares the prefix, no match
     c1, c2 = _tm_pair(W, 12)
-    data = np.concatenate([_rand(2 * W + 5, 21), c2, _rand(3 * W, 22), c1, _rand(W, 23)])
+    data = np.concatenate([_rand(2 * W + 5, 21), c2, _rand(3 * W, 22), c2, _rand(W, 23)])
     key = oracle.digest(c2)
-    wrong = bytes(oracle.sha1(c1)[:16])  # c1's prefix under the shared key
+    wrong = bytes(oracle.sha1(_rand(W, 24))[:16])  # no window of the stream has it
     seeds = [(wrong, key, W)]
     want = oracle.chunk(data, W, seeds=seeds)
     assert not [r for r in want if r[0] == "D"]

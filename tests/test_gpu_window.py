@@ -48,6 +48,7 @@ def _feed(bc, data, rng, max_piece, check_payload=True):
                 for r in (recs[0], recs[-1]):
                     o, n = int(r["offset"]), int(r["size"])
                     assert bc.read_stream(o, n) == data[o:o + n].tobytes()
+                    assert bc.stream_data(o, n) == data[o:o + n].tobytes()  # zero-copy view
             hbm.append(bc.stats()["hbm_bytes"])
     bc.finish()
     taken.append(bc.take_records())

@@ -52,6 +52,7 @@ KERNEL32(k_pk_mad, "v_pk_mad_u16 %0, %0, %1, %2")
 KERNEL32(k_pk_fma, "v_pk_fma_f16 %0, %0, %1, %2")
 KERNEL32(k_fma, "v_fma_f32 %0, %0, %1, %2")
 KERNEL32(k_cvt_pk, "v_cvt_pk_u8_f32 %0, %1, 1, %0")
+KERNEL32(k_bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca")
 
 #define KERNEL64(NAME, ASM)                                                               \
   __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed) {             \
@@ -97,7 +98,7 @@ int main() {
             {"v_or3_b32", k_or3, 1}, {"v_lshl_or_b32", k_lshl_or, 1}, {"v_add_u32_e64", k_add_e64, 1},
             {"v_mad_u32_u16", k_mad_u16, 1}, {"v_dot2_u32_u16", k_dot2, 1}, {"v_mul_hi_u32", k_mul_hi, 1},
             {"v_pk_mad_u16", k_pk_mad, 1}, {"v_pk_fma_f16", k_pk_fma, 1}, {"v_fma_f32", k_fma, 1},
-            {"v_cvt_pk_u8_f32", k_cvt_pk, 1},
+            {"v_cvt_pk_u8_f32", k_cvt_pk, 1}, {"v_bitop3_b32", k_bitop3, 1},
             {"v_lshl_add_u64", k_lshl_add64, 1},
             {"v_mad_u64_u32", k_mad64, 1}};
   const int blocks = cus * 8, tpb = 256;

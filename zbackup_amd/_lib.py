@@ -19,7 +19,7 @@ EXPORTS = ["zc_create", "zc_destroy", "zc_seed_index", "zc_get_input_buffer",
            "zc_chunk_device", "zc_record_count", "zc_get_records", "zc_get_stats", "zc_reset",
            "zc_last_error", "zc_fill_splitmix64", "zc_abi_version", "zc_read_stream", "zc_chunk_host",
            "zc_forget_stream_chunks", "zc_set_window", "zc_get_window", "zc_take_records", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl",
-           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_compress_host", "zc_lzo_last_stats", "zc_adler32", "zc_serialize_records"]
+           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_compress_host", "zc_lzo_last_stats", "zc_adler32", "zc_serialize_records", "zc_stream_data"]
 
 
 class ZcRecord(ctypes.Structure):
@@ -97,6 +97,7 @@ def load(path=LIB_PATH):
         "zc_adler32": (i32, [vp, vp, vp, vp, sz, vp]),
         "zc_serialize_records": (i32, [vp, vp, sz, vp, sz, ctypes.POINTER(sz)]),
         "zc_lzo_last_stats": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]),
+        "zc_stream_data": (vp, [vp, u64, sz]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -204,6 +204,12 @@ class BackupCreator:
                "zc_read_stream")
         return buf.tobytes()
 
+    def stream_data(self, offset, n):
+        """zc_stream_data: the bytes from the feed window's host mirror without a
+        library-side copy (None when they are not in host memory)."""
+        p = self._L.zc_stream_data(self._ctx, offset, n)
+        return ctypes.string_at(p, n) if p else None
+
     def get_backup_data(self):
         """Serialized BackupInstruction stream; like the reference, only once."""
         if self._data_taken:

@@ -175,8 +175,12 @@ hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint6
                        unsigned long long* counters, hipStream_t s);
 // the same in pieces: full 2 MiB tiles [tile0, tile0 + ntiles), then the
 // partial last tile (if any); the pieces may run as the stream arrives
+// beside: the 128-VGPR variant, for a scan that shares the CUs with the grid
+// SHA-1 (ZC_FLAG_SHA1): two waves of each kernel fit on every SIMD whichever is
+// dispatched first (the 137-VGPR scan cannot find room once the SHA-1 waves hold
+// the CUs, and then waits for them: 5.9 instead of 1.6 ms per 8 GiB)
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
-                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s);
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s, bool beside);
 hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                             unsigned long long* counters, hipStream_t s);
 

@@ -384,6 +384,9 @@ struct zc_ctx {
   DevBuf<uint32_t> otiles, obase;
   DevBuf<unsigned long long> counters;
   DevBuf<uint8_t> gsha;  // SHA-1 of the first epoch's grid chunks (ZC_FLAG_SHA1)
+  HostBuf<uint8_t> h_gsha;  // ... copied back on the SHA-1 stream right behind the kernel
+  HostBuf<uint64_t> h_hmkey;  // pinned staging of the keys and anchors of new historic entries
+  HostBuf<uint32_t> h_hmanc;
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
   DevBuf<uint32_t> c_anc, c_g;
   DevBuf<uint8_t> c_dead;
@@ -595,8 +598,9 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
+      // with chunk ids of a whole-stream run the grid SHA-1 shares the CUs
       HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
-                            c_.stream));
+                            c_.stream, !windowed_ && (c_.flags & ZC_FLAG_SHA1)));
       tiles_done_ = t1;
     }
   }
@@ -739,11 +743,14 @@ class Resolver {
     h2d(c_, c_.va.p, starts.data(), k);
     HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, k, W_, pow257(W_), c_.hm_key.p, c_.hanc.p + e0, c_.hg.p + e0,
                         c_.hfp.p + e0, c_.stream));
-    c_.hkey.resize((size_t)e0 + k);
-    hp.anc.resize(k);
-    d2h(c_, c_.hkey.data() + e0, c_.hm_key.p, k);
-    d2h(c_, hp.anc.data(), c_.hanc.p + e0, k);
+    c_.h_hmkey.ensure(k);
+    c_.h_hmanc.ensure(k);
+    d2h(c_, c_.h_hmkey.p, c_.hm_key.p, k);
+    d2h(c_, c_.h_hmanc.p, c_.hanc.p + e0, k);
     sync(c_);
+    c_.hkey.resize((size_t)e0 + k);
+    memcpy(c_.hkey.data() + e0, c_.h_hmkey.p, k * sizeof(uint64_t));
+    hp.anc.assign(c_.h_hmanc.p, c_.h_hmanc.p + k);
     c_.nhist = e0 + k;
     hist_table(c_, e0);
     hp.e0 = e0;
@@ -2040,18 +2047,13 @@ class Resolver {
   // SHA-1 kernel needs no LDS, so it shares the CUs with the scan's
   // workgroups); finalize() takes every record that is one of them from there
   uint64_t pre_sha_n_ = 0;
-  std::vector<uint8_t> gsha_h_;  // the grid chunks' SHA-1 on the host, once needed
   bool gsha_ready_ = false;
   const uint8_t* grid_sha() {
     if (!gsha_ready_) {
-      gsha_h_.resize(pre_sha_n_ * 20);
-      if (pre_sha_n_) {
-        HCK(hipMemcpyAsync(gsha_h_.data(), c_.gsha.p, gsha_h_.size(), hipMemcpyDeviceToHost, c_.sha_stream));
-        HCK(hipStreamSynchronize(c_.sha_stream));
-      }
+      if (pre_sha_n_) HCK(hipStreamSynchronize(c_.sha_stream));  // the kernel and the copy behind it
       gsha_ready_ = true;
     }
-    return gsha_h_.data();
+    return c_.h_gsha.p;
   }
   // grid chunk q's SHA-1 when window [ws, ws + W) is that chunk, else null
   const uint8_t* grid_sha_of(uint64_t ws) {
@@ -2067,9 +2069,11 @@ class Resolver {
     const uint64_t k = (n_ + W_ - 1) / W_;
     if (k > 0xFFFFFFFFull) return;
     c_.gsha.ensure(k * 20);
+    c_.h_gsha.ensure(k * 20);
     HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
     HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
     HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+    HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
     pre_sha_n_ = k;
   }
 
@@ -2668,6 +2672,14 @@ int zc_read_stream(const zc_ctx* c, uint64_t offset, size_t n, void* host_out) {
   hipError_t e = hipMemcpy(host_out, c->d_last + offset, n, hipMemcpyDeviceToHost);
   if (prev >= 0) (void)hipSetDevice(prev);
   return e == hipSuccess ? ZC_OK : ZC_ERR_HIP;
+}
+
+const void* zc_stream_data(const zc_ctx* c, uint64_t offset, size_t n) {
+  if (!c) return nullptr;
+  ZC_LOCK(c);
+  if (!c->windowed_last || !c->hwin.p || offset < c->wbase || offset > c->wend || n > c->wend - offset)
+    return nullptr;
+  return c->hwin.p + (offset - c->wbase);
 }
 
 // Message::serialize of BackupInstruction (message.cc:16-23, zbackup.proto:149-159): a

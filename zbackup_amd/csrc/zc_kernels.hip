@@ -2287,8 +2287,10 @@ __device__ __forceinline__ void sha1_range(const uint8_t* __restrict__ data, uin
   if ((base & 15) == 0) {
     // aligned ranges (every grid chunk): 16-byte loads, kAhead blocks in
     // flight while the current one is hashed (one block of SHA-1 is shorter
-    // than HBM's latency under load)
-    constexpr uint32_t kAhead = 4;
+    // than HBM's latency under load).  Two, not four: 81 VGPRs instead of 146,
+    // so two SHA-1 waves fit on a SIMD beside the scan's two
+    // (tools/ubench/overlap_bench.hip: alone 2.59 vs 2.72 ms per 8 GiB)
+    constexpr uint32_t kAhead = 2;
     const uint4* p = (const uint4*)(data + base);
     uint4 nx[kAhead][4] = {};
 #pragma unroll
@@ -2412,11 +2414,15 @@ static int cu_count() {
 }
 
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
-                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s, bool beside) {
   if (!ntiles) return hipSuccess;
   const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
-  hipLaunchKernelGGL(zc_scan_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles, anchor_lo, blk,
-                     po, counters);
+  if (beside)
+    hipLaunchKernelGGL(zc_scan_kernel_v128<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), sizeof(ScanLds), s, data, n,
+                       tile0, ntiles, anchor_lo, blk, po, counters);
+  else
+    hipLaunchKernelGGL(zc_scan_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles,
+                       anchor_lo, blk, po, counters);
   return hipGetLastError();
 }
 
@@ -2430,7 +2436,7 @@ hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, 
 
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s) {
-  hipError_t e = launch_scan_tiles(data, n, 0, n / ZC_STILE, anchor_lo, blk, po, counters, s);
+  hipError_t e = launch_scan_tiles(data, n, 0, n / ZC_STILE, anchor_lo, blk, po, counters, s, false);
   if (e != hipSuccess) return e;
   return launch_scan_tail(data, n, anchor_lo, blk, po, counters, s);
 }
