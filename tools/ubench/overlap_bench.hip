@@ -79,46 +79,45 @@ int main(int argc, char** argv) {
   CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
   hipEvent_t a, b, e1, e2; CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
   using ScanK = void (*)(const uint8_t*, uint64_t, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*);
-  using ShaK = void (*)(const uint8_t*, uint32_t, uint32_t, uint8_t*);
   constexpr int P = kScanProduct;
-  struct Arm { const char* name; ScanK scan; ShaK sha; int sha_first; std::vector<float> t; };
+  uint32_t *hanc, *hg; uint64_t* hfp;
+  CK(hipMalloc(&hanc, (size_t)nr * 16)); CK(hipMalloc(&hg, (size_t)nr * 16)); CK(hipMalloc(&hfp, (size_t)nr * 32));
+  // arms: scan variant (or none), SHA (product lean grid kernel), heads (product)
+  struct Arm { const char* name; ScanK scan; bool v128; bool sha; bool heads; std::vector<float> t; };
   std::vector<Arm> arms = {
-    {"scan alone", zc_scan_kernel<P>, nullptr, 0, {}},
-    {"scan<=128 alone", zc_scan_kernel_v128<P>, nullptr, 0, {}},
-    {"sha a4 alone", nullptr, sha_v<4, 1>, 0, {}},
-    {"sha a2 alone", nullptr, sha_v<2, 1>, 0, {}},
-    {"sha a2<=128 alone", nullptr, sha_v<2, 4>, 0, {}},
-    {"sha a1<=96 alone", nullptr, sha_v<1, 5>, 0, {}},
-    {"scan + sha a4", zc_scan_kernel<P>, sha_v<4, 1>, 0, {}},
-    {"scan + sha a2", zc_scan_kernel<P>, sha_v<2, 1>, 0, {}},
-    {"scan<=128 + sha a2<=128", zc_scan_kernel_v128<P>, sha_v<2, 4>, 0, {}},
-    {"scan<=128 + sha a4<=128", zc_scan_kernel_v128<P>, sha_v<4, 4>, 0, {}},
-    {"scan<=128 + sha a1<=96", zc_scan_kernel_v128<P>, sha_v<1, 5>, 0, {}},
-    {"sha a2<=128 first, scan<=128", zc_scan_kernel_v128<P>, sha_v<2, 4>, 1, {}},
-    {"scan then sha a4 (serial)", zc_scan_kernel<P>, sha_v<4, 1>, 2, {}},
+    {"scan alone", zc_scan_kernel<P>, false, false, false, {}},
+    {"scan prio alone", zc_scan_kernel<P | ABL_PRIO>, false, false, false, {}},
+    {"sha grid16 alone", nullptr, false, true, false, {}},
+    {"heads alone", nullptr, false, false, true, {}},
+    {"scan + heads", zc_scan_kernel<P>, false, false, true, {}},
+    {"scan prio + heads", zc_scan_kernel<P | ABL_PRIO>, false, false, true, {}},
+    {"scan + sha", zc_scan_kernel<P>, false, true, false, {}},
+    {"scan prio + sha", zc_scan_kernel<P | ABL_PRIO>, false, true, false, {}},
+    {"scan v128 + sha", zc_scan_kernel_v128<P>, true, true, false, {}},
+    {"scan v128 prio + sha", zc_scan_kernel_v128<P | ABL_PRIO>, true, true, false, {}},
+    {"scan + sha + heads", zc_scan_kernel<P>, false, true, true, {}},
+    {"scan prio + sha + heads", zc_scan_kernel<P | ABL_PRIO>, false, true, true, {}},
   };
   const unsigned sgrid = (unsigned)std::min<uint64_t>(ntiles, cus);
+  hipStream_t s3;
+  CK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+  hipEvent_t e3; CK(hipEventCreate(&e3));
   for (int round = 0; round < 12; ++round)
     for (auto& v : arms) {
       CK(hipMemsetAsync(cnt, 0, 64, s1));
       CK(hipStreamSynchronize(s1));
       CK(hipEventRecord(a, s1));
       CK(hipStreamWaitEvent(s2, a, 0));
-      const size_t dyn = v.scan == (ScanK)zc_scan_kernel_v128<P> ? sizeof(ScanLds) : 0;
-      auto scan = [&] { hipLaunchKernelGGL(v.scan, dim3(sgrid), dim3(ZC_SCAN_TPB), dyn, s1, d, n, (uint64_t)0, ntiles, anchor_lo_for(W), blk, po, cnt); };
-      auto sha = [&](hipStream_t s) { hipLaunchKernelGGL(v.sha, dim3((nr + 63) / 64), dim3(64), 0, s, d, W, nr, out); };
-      if (v.sha_first == 2) {
-        scan();
-        sha(s1);
-      } else if (v.sha_first == 1) {
-        sha(s2);
-        if (v.scan) scan();
-      } else {
-        if (v.scan) scan();
-        if (v.sha) sha(s2);
-      }
+      CK(hipStreamWaitEvent(s3, a, 0));
+      if (v.scan)
+        hipLaunchKernelGGL(v.scan, dim3(sgrid), dim3(ZC_SCAN_TPB), v.v128 ? sizeof(ScanLds) : 0, s1, d, n, (uint64_t)0,
+                           ntiles, anchor_lo_for(W), blk, po, cnt);
+      if (v.sha) CK(launch_sha1_grid(d, n, W, nr, out, s2));
+      if (v.heads) CK(launch_grid_heads(d, n, 0, nr - 1, W, anchor_lo_for(W), hanc, hg, hfp, s3));
       CK(hipEventRecord(e2, s2));
+      CK(hipEventRecord(e3, s3));
       CK(hipStreamWaitEvent(s1, e2, 0));
+      CK(hipStreamWaitEvent(s1, e3, 0));
       CK(hipEventRecord(b, s1)); CK(hipEventSynchronize(b));
       float ms; CK(hipEventElapsedTime(&ms, a, b));
       if (round) v.t.push_back(ms);
