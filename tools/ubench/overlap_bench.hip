@@ -86,6 +86,8 @@ int main(int argc, char** argv) {
   struct Arm { const char* name; ScanK scan; bool v128; bool sha; bool heads; std::vector<float> t; };
   std::vector<Arm> arms = {
     {"scan alone", zc_scan_kernel<P>, false, false, false, {}},
+    {"scan perbyte alone", zc_scan_kernel<P | ABL_PERBYTE>, false, false, false, {}},
+    {"scan perbyte + sha", zc_scan_kernel<P | ABL_PERBYTE>, false, true, false, {}},
     {"scan prio alone", zc_scan_kernel<P | ABL_PRIO>, false, false, false, {}},
     {"sha grid16 alone", nullptr, false, true, false, {}},
     {"heads alone", nullptr, false, false, true, {}},

@@ -206,7 +206,8 @@ enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, 
        ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128, ABL_TE_DIGEST_ONLY = 256,
        ABL_DMA_NT = 512, ABL_DMA_SC1 = 1024, ABL_STAGGER_HALF = 2048, ABL_STAGGER_QUARTER = 4096,
        ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768,
-       ABL_TE_DIGEST_NT = 65536, ABL_TE_DIGEST_SAME = 131072, ABL_PRIO = 262144 };
+       ABL_TE_DIGEST_NT = 65536, ABL_TE_DIGEST_SAME = 131072, ABL_PRIO = 262144,
+       ABL_PERBYTE = 524288 /* timing only: the per-byte gear of round 2 (every position tested) */ };
 // the product's scan: the staging DMA is non-temporal (the stream is read
 // once; tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB)
 constexpr int kScanProduct = ABL_DMA_NT;
@@ -248,7 +249,16 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t x = xs[d];
-    if (!(ABL & ABL_NO_GEAR)) {
+    if ((ABL & ABL_PERBYTE) && !(ABL & ABL_NO_GEAR)) {
+      const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
+                              __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
+                              __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
+      int32_t gk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gk[k] = (int32_t)((s.glo << (k + 1)) + dd[k]);
+      s.glo = (uint32_t)gk[3];
+      gd[d] = max(max(gk[0], gk[1]), max(gk[2], gk[3]));
+    } else if (!(ABL & ABL_NO_GEAR)) {
       s.glo = (s.glo << 4) + __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false);
       gd[d] = (int32_t)s.glo;
     }
@@ -1043,9 +1053,11 @@ __global__ void __launch_bounds__(256) zc_heads_kernel(const uint8_t* __restrict
                                                        uint32_t cnt, uint32_t W, int32_t lo_thr,
                                                        uint32_t* __restrict__ anc_off, uint32_t* __restrict__ cg,
                                                        uint64_t* __restrict__ cfp) {
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
-  if (wave >= cnt) return;
+  // persistent waves (a few per SIMD, so kernels queued beside this one --
+  // the epoch's copies -- still find room), each over chunks w, w + nw, ...
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < cnt; wave += nw) {
   const uint32_t i = (uint32_t)wave;
   const uint64_t c = starts ? starts[i] : r_e + (uint64_t)i * W;
   const uint32_t rho0 = (3u - (uint32_t)c) & 3u;
@@ -1132,6 +1144,7 @@ __global__ void __launch_bounds__(256) zc_heads_kernel(const uint8_t* __restrict
     anc_off[4 * (uint64_t)i + rho] = o;
     cg[4 * (uint64_t)i + rho] = o == ZC_NO_ANCHOR ? 0u : gg;
     cfp[4 * (uint64_t)i + rho] = o == ZC_NO_ANCHOR ? 0ull : anchor_fp(data, c + o);
+  }
   }
 }
 
@@ -2660,6 +2673,11 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
 
 
 
+// zc_heads: 4 waves per block, at most 2 blocks per CU (8 waves per CU)
+static unsigned heads_blocks(uint64_t chunks) {
+  return (unsigned)std::min<uint64_t>(blocks_for(64ull * chunks, 256), (uint64_t)cu_count() * 2);
+}
+
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
                               hipStream_t s) {
@@ -2675,7 +2693,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
   // the grid chunks' anchors of the other three residues, unless computed
   // already (the first epoch's, beside the scan)
   if (nsref && !ix.heads_ready)
-    hipLaunchKernelGGL(zc_heads_kernel, dim3(blocks_for(64ull * nsref, 256)), dim3(256), 0, s, data, n,
+    hipLaunchKernelGGL(zc_heads_kernel, dim3(heads_blocks(nsref)), dim3(256), 0, s, data, n,
                        (const uint64_t*)nullptr, r_e, nsref, W, ix.lo_thr, ix.anc + 4ull * nconf, ix.cg + 4ull * nconf,
                        ix.cfp + 4ull * nconf);
   if (!nref) return hipGetLastError();
@@ -2707,7 +2725,7 @@ hipError_t launch_ref_meta(const uint8_t* data, uint64_t n, const uint64_t* blk,
   if (!cnt) return hipSuccess;
   hipLaunchKernelGGL(zc_ref_meta_kernel, dim3(blocks_for(cnt, 128)), dim3(128), 0, s, data, blk, av, starts, cnt, W, pw,
                      key, anc_off, cg, cfp);
-  hipLaunchKernelGGL(zc_heads_kernel, dim3(blocks_for(64ull * cnt, 256)), dim3(256), 0, s, data, n, starts, 0ull, cnt,
+  hipLaunchKernelGGL(zc_heads_kernel, dim3(heads_blocks(cnt)), dim3(256), 0, s, data, n, starts, 0ull, cnt,
                      W, lo_thr, anc_off, cg, cfp);
   return hipGetLastError();
 }
@@ -2724,7 +2742,7 @@ hipError_t launch_ref_gather(const uint32_t* src, const uint32_t* dst, uint32_t 
 hipError_t launch_grid_heads(const uint8_t* data, uint64_t n, uint64_t r_e, uint32_t cnt, uint32_t W, int32_t lo_thr,
                              uint32_t* anc_off, uint32_t* cg, uint64_t* cfp, hipStream_t s) {
   if (!cnt) return hipSuccess;
-  hipLaunchKernelGGL(zc_heads_kernel, dim3(blocks_for(64ull * cnt, 256)), dim3(256), 0, s, data, n,
+  hipLaunchKernelGGL(zc_heads_kernel, dim3(heads_blocks(cnt)), dim3(256), 0, s, data, n,
                      (const uint64_t*)nullptr, r_e, cnt, W, lo_thr, anc_off, cg, cfp);
   return hipGetLastError();
 }
