@@ -56,32 +56,24 @@ constexpr uint64_t ZC_FWT = 64ull * ZC_FLSPAN;
 static_assert(ZC_FWT % ZC_TILE == 0, "screen wave-tiles cover whole zc_fscan tiles");
 constexpr uint32_t ZC_FWT_OVERFLOW = 0xFFFFFFFFu;            // wave-tile left for zc_fscan
 
-// Content anchors.  gear(q) = sum_{j<32} b[q-j] * 2^j (mod 2^32), sampled at
-// dword ends: q is an anchor iff q = 3 (mod 4) (absolute stream offset) and
-// (int32)gear(q) >= anchor_lo, i.e. gear in [anchor_lo, 0x7FFFFFFF] -- 1 sampled
-// position in rate_inv / 4 for random bytes, so 1 byte position in rate_inv
-// (rate_inv = 2^32 / (2^31 - anchor_lo) * 4, chosen per stream from W so a
-// W-byte chunk holds ~16 anchors); never inside a run of one repeated byte
-// (gear 0 or -c).  Sampling makes anchors depend on the alignment: a window
-// at w sees content offsets o = 3 - w (mod 4) only.  So a chunk (ref) keeps
-// one anchor per content-offset residue rho (ZC_ANCHOR_RES of them): its first
-// anchor at offset >= ZC_ANCHOR_MIN_OFF with o = rho (mod 4) -- the residue of
-// its own alignment from the scan's pool, the other three from its bytes
-// (zc_heads_kernel) -- and every residue enters the anchor table.  The table
-// key is the gear value, confirmed by a 64-bit fingerprint of the 8 bytes
-// ending at the anchor.  Per-ref arrays hold ZC_ANCHOR_RES entries per ref
-// (index 4 ref + rho).
+// Content anchors.  gear(q) = sum_{j<32} b[q-j] * 2^j (mod 2^32); q is an
+// anchor iff (int32)gear(q) >= anchor_lo, i.e. gear in [anchor_lo, 0x7FFFFFFF]:
+// 1 position in rate_inv for random bytes (rate_inv = 2^32 / (2^31 - anchor_lo),
+// chosen per stream from W so a W-byte chunk holds ~16 anchors), never inside a
+// run of one repeated byte (gear 0 or -c).  Every position is tested, so a
+// window holds the anchors of its content at any alignment.  A chunk's anchor
+// is its first one at offset >= ZC_ANCHOR_MIN_OFF; the table key is the gear
+// value, confirmed by a 64-bit fingerprint of the 8 bytes ending at the anchor.
 constexpr uint32_t ZC_ANCHOR_MIN_OFF = 63;
 constexpr uint32_t ZC_NO_ANCHOR = 0xFFFFFFFFu;
-constexpr uint32_t ZC_ANCHOR_RES = 4;
 
-inline uint32_t anchor_rate_inv(uint32_t W) {  // byte positions per anchor
+inline uint32_t anchor_rate_inv(uint32_t W) {
   uint32_t rate_inv = 16;
   while (rate_inv < 4096 && rate_inv * 2 <= W / 16) rate_inv *= 2;
   return rate_inv;
 }
-inline int32_t anchor_lo_for(uint32_t W) {  // per sampled position: 4 / rate_inv
-  return (int32_t)(0x80000000u - (uint32_t)(0x400000000ull / anchor_rate_inv(W)));
+inline int32_t anchor_lo_for(uint32_t W) {
+  return (int32_t)(0x80000000u - (uint32_t)(0x100000000ull / anchor_rate_inv(W)));
 }
 
 // Anchors of the stream, per wave-tile t: cnt[t] anchors, sorted by position,
@@ -215,9 +207,6 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
 //      two such grid chunks are not byte-checked: they are counted in
 //      counters[CNT_SPAIRS] and decided by launch_class_sha once the SHA-1
 //      has been computed.
-// Per-ref anchor arrays (cg, cfp, anc) hold ZC_ANCHOR_RES entries per ref
-// (index 4 ref + rho); the grid chunks' are filled by chunk_meta (the residue
-// the scan's pool holds) and zc_heads (the others) unless heads_ready.
 // Refs [0, nconf) must have start/key/cg/cfp/anc uploaded (vis = 0, dead = 0).
 // The class table has 2^cbits >= 2 nref slots, the anchor table 2^tbits
 // (2 << tbits words of tab; tab may be null when the stream has no anchors).
@@ -240,8 +229,6 @@ struct EpochIndex {
   uint2* pairs;  // scratch: nref {ref, leader} pairs for the byte check
   const uint8_t* gsha;  // null: every pair by bytes
   uint64_t n_gsha;
-  int32_t lo_thr;    // the stream's anchor threshold (anchor_lo_for)
-  bool heads_ready;  // the grid chunks' other-residue anchors are in cg/cfp/anc already
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
@@ -253,21 +240,15 @@ hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, ui
                             uint32_t nref, hipStream_t s);
 uint32_t probe_filter_words();
 
-// key and the four residues' first anchors of chunks [starts[i], starts[i] + W)
-// (resident): key[i], anc_off/cg/cfp[4 i + rho]
-hipError_t launch_ref_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, const uint64_t* starts,
-                           uint32_t cnt, uint32_t W, uint64_t pw, int32_t lo_thr, uint64_t* key, uint32_t* anc_off,
-                           uint32_t* cg, uint64_t* cfp, hipStream_t s);
-// key[dst[t]] = ckey[src[t]], anchors 4 dst[t] + rho = 4 src[t] + rho (t < cnt): chunks
-// joining the historic index whose metadata an epoch computed (its refs)
+// key and first anchor of chunks [starts[i], starts[i] + W) (resident)
+hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView av, const uint64_t* starts,
+                           uint32_t cnt, uint32_t W, uint64_t pw, uint64_t* key, uint32_t* anc_off, uint32_t* cg,
+                           uint64_t* cfp, hipStream_t s);
+// key, first anchor, gear and fingerprint of entry dst[t] = those of ref src[t]
+// (t < cnt): chunks joining the historic index whose metadata an epoch computed
 hipError_t launch_ref_gather(const uint32_t* src, const uint32_t* dst, uint32_t cnt, const uint64_t* ckey,
                              const uint32_t* canc, const uint32_t* cg, const uint64_t* cfp, uint64_t* key,
                              uint32_t* anc, uint32_t* g, uint64_t* fp, hipStream_t s);
-// the anchors of the residues the scan's pool does not hold, of the grid chunks
-// r_e + i W (i < cnt), into slots 4 i + rho (the first epoch's, beside the scan)
-hipError_t launch_grid_heads(const uint8_t* data, uint64_t n, uint64_t r_e, uint32_t cnt, uint32_t W, int32_t lo_thr,
-                             uint32_t* anc_off, uint32_t* cg, uint64_t* cfp, hipStream_t s);
-
 // The historic index: entries whose bytes have left HBM, {key, SHA-1 prefix}
 // on the host, {first anchor offset, gear, fingerprint} on the device; those
 // with an anchor sit in an anchor table of the epoch table's layout
@@ -276,10 +257,9 @@ struct HistTab {
   const uint64_t* tab;  // null: no historic entry has an anchor
   uint32_t bits;
   const uint32_t* filt;
-  const uint32_t* anc;  // first anchor offset per entry and residue (4 e + rho)
+  const uint32_t* anc;  // first anchor offset per entry
 };
-// the anchors (4 e + rho) of entries [e0, e0 + cnt) of g / fp / anc into the table
-// and its filter
+// entries [e0, e0 + cnt) of g / fp with an anchor (anc) into the table and its filter
 hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, const uint32_t* anc, uint32_t e0, uint32_t cnt,
                               uint64_t* tab, uint32_t bits, uint32_t* filt, hipStream_t s);
 // after the window slid by `shift` pool entries: directory entries [0, cnt)

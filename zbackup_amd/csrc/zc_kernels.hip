@@ -207,7 +207,7 @@ enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, 
        ABL_DMA_NT = 512, ABL_DMA_SC1 = 1024, ABL_STAGGER_HALF = 2048, ABL_STAGGER_QUARTER = 4096,
        ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768,
        ABL_TE_DIGEST_NT = 65536, ABL_TE_DIGEST_SAME = 131072, ABL_PRIO = 262144,
-       ABL_PERBYTE = 524288 /* timing only: the per-byte gear of round 2 (every position tested) */ };
+       ABL_DWORD_SAMPLED = 524288 /* timing only: anchors tested at dword ends only */ };
 // the product's scan: the staging DMA is non-temporal (the stream is read
 // once; tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB)
 constexpr int kScanProduct = ABL_DMA_NT;
@@ -223,19 +223,21 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// One 16-byte piece of the scan (four dwords).  Gear: the content anchors are
-// sampled at dword ends (stream positions q = 3 mod 4), where the gear of the
-// 32 bytes ending at q is g(q) = (g(q - 4) << 4) + (8 b0 + 4 b1 + 2 b2 + b3):
-// one v_dot4_u32_u8 and one shift-add per dword (the refs' side keeps an
-// anchor per content-offset residue, so a window at any alignment still finds
-// one: zc_heads_kernel).  Digest: two bytes per step, acc*257^2 + (257 b_0 +
-// b_1) (v_perm + SDWA add for the pair, two v_mad_u64_u32 for the 64-bit
-// multiply-add).  Anchor test: the max of the piece's four sampled gears, one
+// One 16-byte piece of the scan (four dwords).  Gear: position k of a dword is
+// g_k = (g << (k+1)) + sum_{j<=k} b_j 2^(k-j), the byte-weighted sums coming
+// from v_dot4_u32_u8, so the four positions are independent of each other.
+// Digest: two bytes per step, acc*257^2 + (257 b_0 + b_1) (v_perm + SDWA
+// add for the pair, two v_mad_u64_u32 for the 64-bit multiply-add).  Anchor
+// test: the max of the piece's sixteen gears (two v_max3 per dword), one
 // compare and one ballot per piece.  The recording block is wave-uniform (the
-// list count stays scalar) and entered for ~22 % of pieces at the 1/4096 anchor
-// rate: each lane with a hit appends the piece (its bytes, the gear before it
-// and a link to the lane's previous entry) to the wave's LDS list, and the tile
-// end re-derives the exact anchors from those 16 bytes.
+// list count stays scalar) and entered for ~22 % of pieces at the 1/4096
+// anchor rate: each lane with a hit appends the piece (its bytes, the gear
+// before it and a link to the lane's previous entry) to the wave's LDS list,
+// and the tile end re-derives the exact anchors from those 16 bytes.
+// (ABL_DWORD_SAMPLED, timing only: the gear tested at dword ends alone -- a
+// quarter of the positions -- saves 6 % of the kernel, but windows at other
+// alignments then need every chunk's anchors in four residues, whose search
+// costs more than that: DESIGN 4.1.)
 template <int ABL>
 __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr, ScanLane& s, WaveList& wl,
                                            uint32_t& last) {
@@ -245,22 +247,26 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
     return;
   }
   const uint32_t g0 = s.glo;  // gear before the piece
-  int32_t gd[4];
+  uint32_t g[4][4];
+  int32_t mx[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t x = xs[d];
-    if ((ABL & ABL_PERBYTE) && !(ABL & ABL_NO_GEAR)) {
+    if ((ABL & ABL_DWORD_SAMPLED) && !(ABL & ABL_NO_GEAR)) {
+      s.glo = (s.glo << 4) + __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false);
+      mx[d] = d == 0 ? (int32_t)s.glo : max(mx[d - 1], (int32_t)s.glo);
+      g[d][3] = s.glo;
+    } else if (!(ABL & ABL_NO_GEAR)) {
       const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
                               __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
                               __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
-      int32_t gk[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) gk[k] = (int32_t)((s.glo << (k + 1)) + dd[k]);
-      s.glo = (uint32_t)gk[3];
-      gd[d] = max(max(gk[0], gk[1]), max(gk[2], gk[3]));
-    } else if (!(ABL & ABL_NO_GEAR)) {
-      s.glo = (s.glo << 4) + __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false);
-      gd[d] = (int32_t)s.glo;
+      for (int k = 0; k < 4; ++k) g[d][k] = (s.glo << (k + 1)) + dd[k];
+      s.glo = g[d][3];
+      // one max3 chain over the piece's 16 gears (8 v_max3_i32 per piece)
+      mx[d] = d == 0 ? max(max((int32_t)g[0][0], (int32_t)g[0][1]), (int32_t)g[0][2])
+                     : max(max(mx[d - 1], (int32_t)g[d - 1][3]), (int32_t)g[d][0]);
+      if (d > 0) mx[d] = max(max(mx[d], (int32_t)g[d][1]), (int32_t)g[d][2]);
     }
     if (!(ABL & ABL_NO_DIGEST)) {
       // two bytes per Horner step: acc*257^2 + (257 b_0 + b_1).  One v_perm
@@ -281,7 +287,7 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
     }
   }
   if (ABL & ABL_NO_GEAR) return;
-  const int32_t m = max(max(gd[0], gd[1]), max(gd[2], gd[3]));
+  const int32_t m = (ABL & ABL_DWORD_SAMPLED) ? mx[3] : max(mx[3], (int32_t)g[3][3]);
   if (ABL & ABL_NO_BRANCH) {
     s.hhi ^= (uint32_t)m;
     return;
@@ -348,7 +354,7 @@ __device__ uint64_t subspan_pass(const uint8_t* __restrict__ data, uint64_t n, u
             const uint32_t b = (xs[d] >> (8 * j)) & 0xFFu;
             gear_step(b, s);
             digest_step(b, s);
-            if ((p & 3) == 3 && (int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) emit(p, s.glo);
+            if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) emit(p, s.glo);
           }
         }
     }
@@ -528,9 +534,14 @@ __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, 
   h.xs[3] = v.w;
   uint32_t g = h.g0, mask = 0;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {  // the sampled positions: dword ends (bit 4 d + 3)
-    g = (g << 4) + __builtin_amdgcn_udot4(h.xs[d], 0x01020408u, 0u, false);
-    mask |= ((int32_t)g >= lo_thr) ? 1u << (4 * d + 3) : 0u;
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t x = h.xs[d];
+    const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
+                            __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
+                            __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mask |= ((int32_t)((g << (k + 1)) + dd[k]) >= lo_thr) ? 1u << (4 * d + k) : 0u;
+    g = (g << 4) + dd[3];
   }
   if (span0 + h.rel < ZC_ANCHOR_MIN_OFF)  // the stream's first 63 positions are no anchors
     mask &= ~0u << min(ZC_ANCHOR_MIN_OFF - (uint32_t)(span0 + h.rel), 16u);
@@ -989,11 +1000,10 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   key[i] = pw + rk_acc(data, blk, c, c + W);
   uint32_t off, gv;
   uint64_t f;
-  first_anchor(data, av, c, W, off, gv, f);  // the residue the pool holds
-  const uint32_t rho0 = (3u - (uint32_t)c) & 3u;
-  anc_off[4 * i + rho0] = off;
-  cg[4 * i + rho0] = gv;
-  cfp[4 * i + rho0] = f;
+  first_anchor(data, av, c, W, off, gv, f);
+  anc_off[i] = off;
+  cg[i] = gv;
+  cfp[i] = f;
 }
 
 // zc_ref_meta: thread per chunk [start[i], start[i] + W) anywhere in the
@@ -1009,157 +1019,38 @@ __global__ void zc_ref_meta_kernel(const uint8_t* __restrict__ data, const uint6
   key[i] = pw + rk_acc(data, blk, c, c + W);
   uint32_t off, gv;
   uint64_t f;
-  first_anchor(data, av, c, W, off, gv, f);  // the residue the pool holds
-  const uint32_t rho0 = (3u - (uint32_t)c) & 3u;
-  anc_off[4 * i + rho0] = off;
-  cg[4 * i + rho0] = gv;
-  cfp[4 * i + rho0] = f;
+  first_anchor(data, av, c, W, off, gv, f);
+  anc_off[i] = off;
+  cg[i] = gv;
+  cfp[i] = f;
 }
 
-// zc_ref_gather: entries e0 + t (t < cnt) of the historic index take ref src[t]
-// of the epoch's arrays (its key, and its four anchors' offset, gear and
-// fingerprint) -- the stream's saved chunks, whose metadata the epoch computed
+// zc_ref_gather: historic entry dst[t] (t < cnt) takes ref src[t] of the
+// epoch's arrays (its key, first anchor offset, gear and fingerprint) -- the
+// stream's saved chunks, whose metadata the epoch computed already
 __global__ void zc_ref_gather_kernel(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst, uint32_t cnt,
                                      const uint64_t* __restrict__ ckey, const uint32_t* __restrict__ canc,
                                      const uint32_t* __restrict__ cgv, const uint64_t* __restrict__ cfpv,
                                      uint64_t* __restrict__ key, uint32_t* __restrict__ anc, uint32_t* __restrict__ g,
                                      uint64_t* __restrict__ fp) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 4 * cnt) return;
-  const uint32_t j = t >> 2, rho = t & 3u, r = src[j], e = dst[j];
-  if (rho == 0) key[e] = ckey[r];
-  anc[4 * (uint64_t)e + rho] = canc[4 * (uint64_t)r + rho];
-  g[4 * (uint64_t)e + rho] = cgv[4 * (uint64_t)r + rho];
-  fp[4 * (uint64_t)e + rho] = cfpv[4 * (uint64_t)r + rho];
+  if (t >= cnt) return;
+  const uint32_t r = src[t], e = dst[t];
+  key[e] = ckey[r];
+  anc[e] = canc[r];
+  g[e] = cgv[r];
+  fp[e] = cfpv[r];
 }
 
-// zc_heads: the anchors of a chunk [c, c + W) that the scan's pool cannot give
-// -- the pool samples stream positions 3 (mod 4), i.e. the chunk's content
-// offsets of one residue rho0 = (3 - c) mod 4 -- read from its bytes: for each
-// other residue rho, the first offset o >= ZC_ANCHOR_MIN_OFF, o = rho (mod 4),
-// o < W, whose gear is an anchor's (ZC_NO_ANCHOR: none), with its gear value and
-// fingerprint, into slot 4 i + rho.  One wave per chunk, 2 KiB per step (32
-// positions per lane, the next step's bytes loaded while this one is hashed)
-// until every residue is found (~2 A bytes for A bytes per anchor: the last of
-// three geometric waits).  A lane reads its own 32 bytes only: the gear before
-// them is the gear of the previous lane's 32 bytes (the gear spans exactly 32
-// bytes), handed over with one shuffle.  starts: the chunks' starts, or null
-// for a grid r_e + i W.
-__device__ __forceinline__ uint4 heads_load(const uint8_t* __restrict__ data, uint64_t n, uint64_t q) {
-  return q + 16 <= n ? *(const uint4*)(data + q) : load16_clamped(data, n, q);
-}
-__global__ void __launch_bounds__(256) zc_heads_kernel(const uint8_t* __restrict__ data, uint64_t n,
-                                                       const uint64_t* __restrict__ starts, uint64_t r_e,
-                                                       uint32_t cnt, uint32_t W, int32_t lo_thr,
-                                                       uint32_t* __restrict__ anc_off, uint32_t* __restrict__ cg,
-                                                       uint64_t* __restrict__ cfp) {
-  const uint32_t lane = threadIdx.x & 63;
-  // persistent waves (a few per SIMD, so kernels queued beside this one --
-  // the epoch's copies -- still find room), each over chunks w, w + nw, ...
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  for (uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < cnt; wave += nw) {
-  const uint32_t i = (uint32_t)wave;
-  const uint64_t c = starts ? starts[i] : r_e + (uint64_t)i * W;
-  const uint32_t rho0 = (3u - (uint32_t)c) & 3u;
-  uint32_t need = 0xFu & ~(1u << rho0);
-  uint32_t res_off[4] = {ZC_NO_ANCHOR, ZC_NO_ANCHOR, ZC_NO_ANCHOR, ZC_NO_ANCHOR};
-  uint32_t res_g[4] = {0, 0, 0, 0};
-  if (W > ZC_ANCHOR_MIN_OFF) {
-    const uint64_t lo = c + ZC_ANCHOR_MIN_OFF, hi = c + W;  // positions [lo, hi)
-    uint64_t base = lo & ~31ull;                            // >= c + 32
-    uint32_t carry;  // the gear of the 32 bytes before base
-    {
-      const uint4 a = heads_load(data, n, base - 32), b = heads_load(data, n, base - 16);
-      const uint32_t xs[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      carry = 0;
-#pragma unroll
-      for (int d = 0; d < 8; ++d) carry = (carry << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
-    }
-    uint4 nx0 = make_uint4(0, 0, 0, 0), nx1 = nx0;
-    if (base + 32u * lane < hi) {
-      nx0 = heads_load(data, n, base + 32u * lane);
-      nx1 = heads_load(data, n, base + 32u * lane + 16);
-    }
-    while (base < hi && need) {
-      const uint64_t q0 = base + 32u * lane;
-      const uint4 v0 = nx0, v1 = nx1;
-      if (q0 + 2048 < hi) {  // the next step's bytes, in flight while this one is hashed
-        nx0 = heads_load(data, n, q0 + 2048);
-        nx1 = heads_load(data, n, q0 + 2048 + 16);
-      }
-      const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      uint32_t gown = 0;  // this lane's 32 bytes from zero: the gear at its last byte
-#pragma unroll
-      for (int d = 0; d < 8; ++d) gown = (gown << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
-      uint32_t g = __shfl_up(gown, 1, 64);
-      if (lane == 0) g = carry;
-      carry = __shfl(gown, 63, 64);
-      // position q0 + 4 d + k has content residue (base - c + k) mod 4: mk[k]
-      // holds the hits at dword offset k, bit d; gk1[k] the gear of the first
-      uint32_t mk[4] = {0, 0, 0, 0}, gk1[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        const uint32_t x = xs[d];
-        const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
-                                __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
-                                __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t gk = (g << (k + 1)) + dd[k];
-          const uint64_t q = q0 + 4 * d + k;
-          const bool hit = (int32_t)gk >= lo_thr && q >= lo && q < hi;
-          gk1[k] = (hit && !mk[k]) ? gk : gk1[k];
-          mk[k] |= hit ? 1u << d : 0u;
-          if (k == 3) g = gk;
-        }
-      }
-      const uint32_t sh = (uint32_t)(base - c) & 3u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t rho = (sh + (uint32_t)k) & 3u;
-        if (!(need & (1u << rho))) continue;
-        const uint64_t bl = __ballot(mk[k] != 0);
-        if (!bl) continue;
-        const uint32_t L = (uint32_t)__builtin_ctzll(bl);
-        const uint32_t dL = __shfl(mk[k] ? (uint32_t)__builtin_ctz(mk[k]) : 0u, (int)L, 64);
-        const uint32_t gL = __shfl(gk1[k], (int)L, 64);
-        const uint32_t o = (uint32_t)(base + 32u * L + 4u * dL + (uint32_t)k - c);
-        res_off[0] = rho == 0 ? o : res_off[0];
-        res_off[1] = rho == 1 ? o : res_off[1];
-        res_off[2] = rho == 2 ? o : res_off[2];
-        res_off[3] = rho == 3 ? o : res_off[3];
-        res_g[0] = rho == 0 ? gL : res_g[0];
-        res_g[1] = rho == 1 ? gL : res_g[1];
-        res_g[2] = rho == 2 ? gL : res_g[2];
-        res_g[3] = rho == 3 ? gL : res_g[3];
-        need &= ~(1u << rho);
-      }
-      base += 2048;
-    }
-  }
-  if (lane < 4 && lane != rho0) {
-    const uint32_t rho = lane;
-    const uint32_t o = rho == 0 ? res_off[0] : rho == 1 ? res_off[1] : rho == 2 ? res_off[2] : res_off[3];
-    const uint32_t gg = rho == 0 ? res_g[0] : rho == 1 ? res_g[1] : rho == 2 ? res_g[2] : res_g[3];
-    anc_off[4 * (uint64_t)i + rho] = o;
-    cg[4 * (uint64_t)i + rho] = o == ZC_NO_ANCHOR ? 0u : gg;
-    cfp[4 * (uint64_t)i + rho] = o == ZC_NO_ANCHOR ? 0ull : anchor_fp(data, c + o);
-  }
-  }
-}
-
-// a ref with a residue that has no anchor is found by its key (the exact
-// screen) for the alignments of that residue
+// a ref without an anchor is found by its key (the exact screen)
 __device__ __forceinline__ bool anc_missing(const uint32_t* __restrict__ anc_off, uint32_t ref) {
-  const uint4 a = *(const uint4*)(anc_off + 4 * (uint64_t)ref);
-  return a.x == ZC_NO_ANCHOR || a.y == ZC_NO_ANCHOR || a.z == ZC_NO_ANCHOR || a.w == ZC_NO_ANCHOR;
+  return anc_off[ref] == ZC_NO_ANCHOR;
 }
 
 // ---------------------------------------------------------------------------
 // anchor table: open addressing on the anchor's gear value, duplicates kept.
-// A slot is 16 bytes, {gear | (4 ref + rho) << 32, fingerprint}: one load
-// gives the key, the ref's anchor of residue rho and the fingerprint to
-// compare (empty: all ones).
+// A slot is 16 bytes, {gear | ref << 32, fingerprint}: one load gives the
+// key, the ref and the fingerprint to compare (empty: all ones).
 constexpr uint64_t kEmpty = ~0ull;
 
 __device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
@@ -1168,7 +1059,7 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
 
 // the probe's first level: bit (g mod 2^kGFiltBits) of every table key (the
 // low bits: an anchor's gear always has its top bits set)
-constexpr int kGFiltBits = 22;                               // 2^22 bits = 512 KiB (4 anchors per ref)
+constexpr int kGFiltBits = 20;                               // 2^20 bits = 128 KiB
 constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
 
 // ---------------------------------------------------------------------------
@@ -1209,9 +1100,9 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
     const uint4 slot = *(const uint4*)(tab + 2 * (uint64_t)h);
     if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
     if (slot.x == gk) {
-      const uint32_t ref = slot.y >> 2;
+      const uint32_t ref = slot.y;
       if (fp == (((uint64_t)slot.w << 32) | slot.z) && cls[ref] == ref) {
-        const uint64_t o = anc_off[slot.y];
+        const uint64_t o = anc_off[ref];
         if (pos >= r + o) {
           const uint64_t ws = pos - o, p = ws + W - 1;
           // a window that is a grid chunk of this epoch in ref's class is the
@@ -1253,8 +1144,8 @@ __device__ __forceinline__ void probe_hist(const uint8_t* __restrict__ data, uin
     const uint4 slot = *(const uint4*)(ht.tab + 2 * (uint64_t)h);
     if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
     if (slot.x == gk && fp == (((uint64_t)slot.w << 32) | slot.z)) {
-      const uint32_t e = slot.y >> 2;
-      const uint64_t o = ht.anc[slot.y];
+      const uint32_t e = slot.y;
+      const uint64_t o = ht.anc[e];
       if (pos >= r + o) {
         const uint64_t p = pos - o + W - 1;
         if (p < n) {
@@ -1443,13 +1334,12 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
                                        const uint32_t* __restrict__ cg, const uint64_t* __restrict__ cfp,
                                        uint32_t nref, uint64_t* ckeys, uint32_t cbits,
                                        uint64_t* tab, uint32_t tbits, uint32_t* __restrict__ gfilt) {
-  // threads [0, nref) insert into the class table, [nref, 5 nref) the refs'
-  // anchors (four residues each) into the anchor table: the CAS chains run
-  // side by side
+  // threads [0, nref) insert into the class table, [nref, 2 nref) into the
+  // anchor table: the two CAS chains run side by side
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 5 * nref) return;
+  if (t >= 2 * nref) return;
   const bool cls_part = t < nref;
-  const uint32_t i = cls_part ? t : t - nref;  // anchor part: slot 4 ref + rho
+  const uint32_t i = cls_part ? t : t - nref;
   // a ref with the same key as the ref before it is not the lowest of its
   // key: only the first ref of each run of equal keys inserts (repeated
   // content -- all-zero streams -- would otherwise serialise every ref on
@@ -1473,7 +1363,7 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
     }
   }
   if (!tab || anc_off[i] == ZC_NO_ANCHOR) return;
-  // every anchor of every ref enters the anchor table (the probe keeps class
+  // every ref with an anchor enters the anchor table (the probe keeps class
   // leaders only: classes are not known yet)
   const uint32_t g = cg[i];
   const uint32_t fb = g & ((1u << kGFiltBits) - 1);
@@ -1495,10 +1385,9 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
 __global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint64_t* __restrict__ fp,
                                       const uint32_t* __restrict__ anc, uint32_t e0, uint32_t cnt, uint64_t* tab,
                                       uint32_t bits, uint32_t* __restrict__ filt) {
-  // thread per anchor slot 4 entry + rho of entries [e0, e0 + cnt)
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 4 * cnt) return;
-  const uint32_t e = 4 * e0 + t, gv = g[e];
+  if (t >= cnt) return;
+  const uint32_t e = e0 + t, gv = g[e];
   if (anc[e] == ZC_NO_ANCHOR) return;
   const uint32_t fb = gv & ((1u << kGFiltBits) - 1);
   atomicOr(&filt[fb >> 5], 1u << (fb & 31));
@@ -2673,11 +2562,6 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
 
 
 
-// zc_heads: 4 waves per block, at most 2 blocks per CU (8 waves per CU)
-static unsigned heads_blocks(uint64_t chunks) {
-  return (unsigned)std::min<uint64_t>(blocks_for(64ull * chunks, 256), (uint64_t)cu_count() * 2);
-}
-
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
                               hipStream_t s) {
@@ -2689,15 +2573,9 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
   const uint64_t threads = std::max<uint64_t>({nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
                      nsref, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
-                     ix.cg + 4ull * nconf, ix.cfp + 4ull * nconf, ix.anc + 4ull * nconf, ec);
-  // the grid chunks' anchors of the other three residues, unless computed
-  // already (the first epoch's, beside the scan)
-  if (nsref && !ix.heads_ready)
-    hipLaunchKernelGGL(zc_heads_kernel, dim3(heads_blocks(nsref)), dim3(256), 0, s, data, n,
-                       (const uint64_t*)nullptr, r_e, nsref, W, ix.lo_thr, ix.anc + 4ull * nconf, ix.cg + 4ull * nconf,
-                       ix.cfp + 4ull * nconf);
+                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ec);
   if (!nref) return hipGetLastError();
-  hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(5ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
+  hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
                      ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
   hipLaunchKernelGGL(zc_class_lead_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, nref,
                      ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.pairs, ix.counters,
@@ -2719,14 +2597,12 @@ hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, ui
 
 uint32_t probe_filter_words() { return kGFiltWords; }
 
-hipError_t launch_ref_meta(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, const uint64_t* starts,
-                           uint32_t cnt, uint32_t W, uint64_t pw, int32_t lo_thr, uint64_t* key, uint32_t* anc_off,
-                           uint32_t* cg, uint64_t* cfp, hipStream_t s) {
+hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView av, const uint64_t* starts,
+                           uint32_t cnt, uint32_t W, uint64_t pw, uint64_t* key, uint32_t* anc_off, uint32_t* cg,
+                           uint64_t* cfp, hipStream_t s) {
   if (!cnt) return hipSuccess;
   hipLaunchKernelGGL(zc_ref_meta_kernel, dim3(blocks_for(cnt, 128)), dim3(128), 0, s, data, blk, av, starts, cnt, W, pw,
                      key, anc_off, cg, cfp);
-  hipLaunchKernelGGL(zc_heads_kernel, dim3(heads_blocks(cnt)), dim3(256), 0, s, data, n, starts, 0ull, cnt,
-                     W, lo_thr, anc_off, cg, cfp);
   return hipGetLastError();
 }
 
@@ -2734,23 +2610,15 @@ hipError_t launch_ref_gather(const uint32_t* src, const uint32_t* dst, uint32_t 
                              const uint32_t* canc, const uint32_t* cg, const uint64_t* cfp, uint64_t* key,
                              uint32_t* anc, uint32_t* g, uint64_t* fp, hipStream_t s) {
   if (!cnt) return hipSuccess;
-  hipLaunchKernelGGL(zc_ref_gather_kernel, dim3(blocks_for(4ull * cnt, 256)), dim3(256), 0, s, src, dst, cnt, ckey, canc,
+  hipLaunchKernelGGL(zc_ref_gather_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, src, dst, cnt, ckey, canc,
                      cg, cfp, key, anc, g, fp);
-  return hipGetLastError();
-}
-
-hipError_t launch_grid_heads(const uint8_t* data, uint64_t n, uint64_t r_e, uint32_t cnt, uint32_t W, int32_t lo_thr,
-                             uint32_t* anc_off, uint32_t* cg, uint64_t* cfp, hipStream_t s) {
-  if (!cnt) return hipSuccess;
-  hipLaunchKernelGGL(zc_heads_kernel, dim3(heads_blocks(cnt)), dim3(256), 0, s, data, n,
-                     (const uint64_t*)nullptr, r_e, cnt, W, lo_thr, anc_off, cg, cfp);
   return hipGetLastError();
 }
 
 hipError_t launch_hist_insert(const uint32_t* g, const uint64_t* fp, const uint32_t* anc, uint32_t e0, uint32_t cnt,
                               uint64_t* tab, uint32_t bits, uint32_t* filt, hipStream_t s) {
   if (!cnt) return hipSuccess;
-  hipLaunchKernelGGL(zc_hist_insert_kernel, dim3(blocks_for(4ull * cnt, 256)), dim3(256), 0, s, g, fp, anc, e0, cnt, tab,
+  hipLaunchKernelGGL(zc_hist_insert_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, g, fp, anc, e0, cnt, tab,
                      bits, filt);
   return hipGetLastError();
 }
