@@ -232,6 +232,10 @@ int zc_adler32(zc_ctx* ctx, const void* d_base, const uint64_t* off, const uint6
 int zc_lzo_last_stats(const zc_ctx* ctx, double* parse_ms, uint64_t* blocks);
 
 int zc_abi_version(void);
+/* digest of the sources this library was built from (zbackup_amd/_build.py
+ * source_digest(): sha256 of every source and header, first 16 hex digits).
+ * Loaders compare it with the checked-out tree and refuse a stale binary. */
+const char* zc_build_id(void);
 
 #ifdef __cplusplus
 }

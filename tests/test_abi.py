@@ -69,3 +69,18 @@ def test_chunk_id_blob_and_framing():
     raw = b"x" * 200
     msg = serialize_instruction(raw=raw)
     assert msg[:4] == bytes([203, 1, 0x12, 200 | 0x80]) and msg[4] == 1 and msg[5:] == raw
+
+
+def test_clean_tree_compiles(tmp_path):
+    """The checked-out sources compile and link (into a temp dir, so a stale
+    in-tree binary cannot hide a tree that does not build)."""
+    out = str(tmp_path / "libzchunk.so")
+    _build.build(force=True, out=out)
+    assert _build.lib_build_id(out) == _build.source_digest()
+
+
+def test_in_tree_library_is_built_from_these_sources(lib):
+    """bench.py, smoke() and the GPU tests load the in-tree library; it must
+    carry the digest of the checked-out sources."""
+    assert _build.lib_build_id() == _build.source_digest()
+    assert _lib.build_id() == _build.source_digest()

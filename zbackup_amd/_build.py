@@ -1,5 +1,7 @@
 """Build libzchunk.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -23,21 +25,43 @@ def hipcc():
     return "hipcc"
 
 
-def stale():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+def source_digest():
+    """sha256 over every source and header the library is built from (and the
+    offload arch), first 16 hex digits: the build id libzchunk.so carries."""
+    h = hashlib.sha256(ARCH.encode())
+    for p in SOURCES + HEADERS:
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
-def build(force=False, verbose=False):
-    if not force and not stale():
-        return LIB
+def lib_build_id(path=LIB):
+    """The build id embedded in a built library (read from the file, without
+    loading it), or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        m = re.search(rb"zc-build-id:([0-9a-f]{16}|unknown)\0", f.read())
+    return m.group(1).decode() if m else None
+
+
+def stale(path=LIB):
+    return lib_build_id(path) != source_digest()
+
+
+def build(force=False, verbose=False, out=LIB):
+    """Compile the library to `out` (in-tree by default) unless it already
+    carries the sources' build id."""
+    if not force and not stale(out):
+        return out
+    bid = source_digest()
+    odir = os.path.dirname(os.path.abspath(out))
     objs, procs = [], []
     for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
         cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
-               "-I" + os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+               "-I" + os.path.join(ROOT, "include"), f'-DZC_BUILD_ID="{bid}"', "-c", src, "-o", obj]
         if os.path.basename(src) in HOST_ONLY:
             cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I" + os.path.join(ROOT, "include"),
                    "-c", src, "-o", obj]
@@ -47,14 +71,21 @@ def build(force=False, verbose=False):
             print(" ".join(cmd), file=sys.stderr)
         procs.append((subprocess.Popen(cmd), cmd))  # the sources compile in parallel
         objs.append(obj)
-    for p, cmd in procs:
-        if p.wait() != 0:
-            raise subprocess.CalledProcessError(p.returncode, cmd)
-    cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+    failed = [(p.returncode, cmd) for p, cmd in procs if p.wait() != 0]
+    if failed:
+        for o in objs:
+            if os.path.exists(o):
+                os.remove(o)
+        raise subprocess.CalledProcessError(*failed[0])
+    tmp = out + ".tmp"
+    cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
     subprocess.run(cmd, check=True)
     for o in objs:
         os.remove(o)
-    return LIB
+    os.replace(tmp, out)  # a failed build never leaves a half-written library
+    if lib_build_id(out) != bid:
+        raise RuntimeError(f"{out}: build id missing after the build")
+    return out
 
 
 if __name__ == "__main__":

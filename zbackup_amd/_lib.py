@@ -19,7 +19,7 @@ EXPORTS = ["zc_create", "zc_destroy", "zc_seed_index", "zc_get_input_buffer",
            "zc_chunk_device", "zc_record_count", "zc_get_records", "zc_get_stats", "zc_reset",
            "zc_last_error", "zc_fill_splitmix64", "zc_abi_version", "zc_read_stream", "zc_chunk_host",
            "zc_forget_stream_chunks", "zc_set_window", "zc_get_window", "zc_take_records", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl",
-           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_compress_host", "zc_lzo_last_stats", "zc_adler32", "zc_serialize_records", "zc_stream_data"]
+           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_compress_host", "zc_lzo_last_stats", "zc_adler32", "zc_serialize_records", "zc_stream_data", "zc_build_id"]
 
 
 class ZcRecord(ctypes.Structure):
@@ -58,6 +58,13 @@ def load(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise ZcError(f"{path} not built (run zbackup_amd/_build.py or __graft_entry__.build())")
+    from . import _build
+    if os.path.abspath(path) == LIB_PATH:
+        # the in-tree library must be the one the checked-out sources build
+        have, want = _build.lib_build_id(path), _build.source_digest()
+        if have != want:
+            raise ZcError(f"{path} has build id {have}, the sources give {want}: stale binary "
+                          "(run zbackup_amd/_build.py)")
     L = ctypes.CDLL(path)
     vp, u32, u64, sz, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int
     sig = {
@@ -98,6 +105,7 @@ def load(path=LIB_PATH):
         "zc_serialize_records": (i32, [vp, vp, sz, vp, sz, ctypes.POINTER(sz)]),
         "zc_lzo_last_stats": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]),
         "zc_stream_data": (vp, [vp, u64, sz]),
+        "zc_build_id": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -105,3 +113,8 @@ def load(path=LIB_PATH):
         fn.argtypes = args
     _lib = L
     return L
+
+
+def build_id():
+    """The build id of the loaded library (the digest of its sources)."""
+    return load().zc_build_id().decode()

@@ -314,7 +314,6 @@ struct zc_ctx {
   hipStream_t sha_stream = nullptr;   // SHA-1 of the grid chunks, beside the scan (ZC_FLAG_SHA1)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   hipEvent_t ev_sha = nullptr;  // the grid chunks' SHA-1 (sha_stream) are complete
-  hipEvent_t ev_heads = nullptr;  // the first epoch's grid chunks' other-residue anchors (copy_stream)
   std::string err;
 
   // host feed
@@ -439,11 +438,6 @@ void sync(zc_ctx& c) { HCK(hipStreamSynchronize(c.stream)); }
 // ---------------------------------------------------------------------------
 // the context's index beyond the stream being resolved
 
-// a chunk with a content-offset residue that has no anchor (4 per chunk)
-inline bool anc_missing(const uint32_t* a) {
-  return a[0] == ZC_NO_ANCHOR || a[1] == ZC_NO_ANCHOR || a[2] == ZC_NO_ANCHOR || a[3] == ZC_NO_ANCHOR;
-}
-
 void add_static(zc_ctx& c, uint64_t key, const uint8_t* sha, uint8_t seeded) {
   StaticEntry e;
   e.key = key;
@@ -495,12 +489,12 @@ void statics_screen(zc_ctx& c) {
   c.sc_ver = c.statics_ver;
 }
 
-// historic table: 2^hbits >= 8 nhist slots (4 anchors per entry); grows by a rebuild, otherwise
+// historic table: 2^hbits >= 2 nhist slots; grows by a rebuild, otherwise
 // entries [from, nhist) are inserted
 void hist_table(zc_ctx& c, uint32_t from) {
   if (!c.nhist) return;
   uint32_t bits = std::max<uint32_t>(c.hbits, 12);
-  while ((1ull << bits) < 8ull * c.nhist) ++bits;  // four anchors per entry
+  while ((1ull << bits) < 2ull * c.nhist) ++bits;
   c.hfilt.ensure(probe_filter_words());
   if (bits != c.hbits || !c.htab.p) {
     sync(c);  // a probe may still read the old table
@@ -646,10 +640,7 @@ class Resolver {
         scan_open_ = true;
       }
       HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.counters.p, c_.stream));
-      if (!windowed_) {
-        pre_sha();
-        pre_heads();
-      }
+      if (!windowed_) pre_sha();
       scan_finish();
       lim_ = n_;
       final_ = true;
@@ -697,9 +688,9 @@ class Resolver {
     hist_add(starts, nullptr);
     cstart_.erase(cstart_.begin(), cstart_.begin() + k);
     ckey_.erase(ckey_.begin(), ckey_.begin() + k);
-    cfp_.erase(cfp_.begin(), cfp_.begin() + 4 * k);
-    cg_.erase(cg_.begin(), cg_.begin() + 4 * k);
-    canc_.erase(canc_.begin(), canc_.begin() + 4 * k);
+    cfp_.erase(cfp_.begin(), cfp_.begin() + k);
+    cg_.erase(cg_.begin(), cg_.begin() + k);
+    canc_.erase(canc_.begin(), canc_.begin() + k);
     nconf_ = (uint32_t)cstart_.size();
   }
 
@@ -745,9 +736,9 @@ class Resolver {
     if (!k || !indexable_) return hp;
     const uint32_t e0 = c_.nhist;
     c_.va.ensure(k);
-    c_.hanc.grow_keep(4ull * (e0 + k), 4ull * e0, c_.stream);  // four residues per entry
-    c_.hg.grow_keep(4ull * (e0 + k), 4ull * e0, c_.stream);
-    c_.hfp.grow_keep(4ull * (e0 + k), 4ull * e0, c_.stream);
+    c_.hanc.grow_keep(e0 + k, e0, c_.stream);
+    c_.hg.grow_keep(e0 + k, e0, c_.stream);
+    c_.hfp.grow_keep(e0 + k, e0, c_.stream);
     c_.hm_key.ensure(k);
     // chunks that are refs of the current epoch take the metadata it computed
     // (its grid chunks, its confirmed refs); the rest is computed from the bytes
@@ -770,34 +761,34 @@ class Resolver {
       h2d(c_, c_.gidx.p, gsrc.data(), m);
       h2d(c_, c_.gidx.p + m, gdst.data(), m);
       HCK(launch_ref_gather(c_.gidx.p, c_.gidx.p + m, m, c_.c_key.p, c_.c_anc.p, c_.c_g.p, c_.c_fp.p, c_.hm_key.p,
-                            c_.hanc.p + 4ull * e0, c_.hg.p + 4ull * e0, c_.hfp.p + 4ull * e0, c_.stream));
+                            c_.hanc.p + e0, c_.hg.p + e0, c_.hfp.p + e0, c_.stream));
     }
     if (!rest.empty()) {
       // computed into the staging slots after the gathered ones, then moved
       const uint32_t m = (uint32_t)rest.size();
-      c_.hm_anc.ensure(4ull * m);
-      c_.hm_g.ensure(4ull * m);
-      c_.hm_fp.ensure(4ull * m);
+      c_.hm_anc.ensure(m);
+      c_.hm_g.ensure(m);
+      c_.hm_fp.ensure(m);
       c_.hm_rkey.ensure(m);
       h2d(c_, c_.va.p, rest.data(), m);
-      HCK(launch_ref_meta(d_, n_, blk_v(), av(), c_.va.p, m, W_, pow257(W_), anchor_lo_, c_.hm_rkey.p, c_.hm_anc.p,
-                          c_.hm_g.p, c_.hm_fp.p, c_.stream));
+      HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, m, W_, pow257(W_), c_.hm_rkey.p, c_.hm_anc.p, c_.hm_g.p,
+                          c_.hm_fp.p, c_.stream));
       std::vector<uint32_t> src(m);
       for (uint32_t t = 0; t < m; ++t) src[t] = t;
       c_.gidx.ensure(2ull * m);
       h2d(c_, c_.gidx.p, src.data(), m);
       h2d(c_, c_.gidx.p + m, rdst.data(), m);
       HCK(launch_ref_gather(c_.gidx.p, c_.gidx.p + m, m, c_.hm_rkey.p, c_.hm_anc.p, c_.hm_g.p, c_.hm_fp.p,
-                            c_.hm_key.p, c_.hanc.p + 4ull * e0, c_.hg.p + 4ull * e0, c_.hfp.p + 4ull * e0, c_.stream));
+                            c_.hm_key.p, c_.hanc.p + e0, c_.hg.p + e0, c_.hfp.p + e0, c_.stream));
     }
     c_.h_hmkey.ensure(k);
-    c_.h_hmanc.ensure(4ull * k);
+    c_.h_hmanc.ensure(k);
     d2h(c_, c_.h_hmkey.p, c_.hm_key.p, k);
-    d2h(c_, c_.h_hmanc.p, c_.hanc.p + 4ull * e0, 4ull * k);
+    d2h(c_, c_.h_hmanc.p, c_.hanc.p + e0, k);
     sync(c_);
     c_.hkey.resize((size_t)e0 + k);
     memcpy(c_.hkey.data() + e0, c_.h_hmkey.p, k * sizeof(uint64_t));
-    hp.anc.assign(c_.h_hmanc.p, c_.h_hmanc.p + 4ull * k);
+    hp.anc.assign(c_.h_hmanc.p, c_.h_hmanc.p + k);
     c_.nhist = e0 + k;
     hist_table(c_, e0);
     hp.e0 = e0;
@@ -812,8 +803,7 @@ class Resolver {
     uint8_t* hs = c_.hsha.data() + 16 * (size_t)hp.e0;
     memcpy(hs, sha16, 16 * (size_t)hp.k);
     for (uint32_t i = 0; i < hp.k; ++i)
-      if (anc_missing(&hp.anc[4 * (size_t)i]))
-        add_static_once(c_, c_.hkey[hp.e0 + i], hs + 16 * (size_t)i, 0);
+      if (hp.anc[i] == ZC_NO_ANCHOR) add_static_once(c_, c_.hkey[hp.e0 + i], hs + 16 * (size_t)i, 0);
   }
 
  private:
@@ -866,8 +856,8 @@ class Resolver {
   // earlier epochs (visible to every later probe), [nconf_, nref_) this
   // epoch's grid chunks, start r_e + k * W, visible from start + 2W - 1.
   // The grid chunks' metadata lives on the device; the host holds their keys.
-  std::vector<uint64_t> cstart_, ckey_, cfp_;  // cfp_: anchor fingerprints (4 per ref: one per residue)
-  std::vector<uint32_t> canc_, cg_;            // cg_: anchor gear values (4 per ref)
+  std::vector<uint64_t> cstart_, ckey_, cfp_;  // cfp_: anchor fingerprint
+  std::vector<uint32_t> canc_, cg_;            // cg_: anchor gear value
   std::vector<uint8_t> dead_;
   uint64_t ndead_ = 0;  // refs of this epoch consumed by same-grid matches
   static constexpr uint64_t kParallelRecords = 32768;
@@ -1088,7 +1078,7 @@ class Resolver {
       EpochIndex ix{};
       const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
       uint32_t tbits = 10;  // sized for every ref having an anchor
-      while ((1u << tbits) < 8u * nref_) ++tbits;  // four anchors per ref
+      while ((1u << tbits) < 2u * nref_) ++tbits;
       if (anchors) {
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         if (nref_) {
@@ -1100,19 +1090,19 @@ class Resolver {
       if (nref_) {
         c_.c_start.ensure(nref_);
         c_.c_key.ensure(nref_);
-        c_.c_fp.ensure(4ull * nref_);
+        c_.c_fp.ensure(nref_);
         c_.c_vis.ensure(nref_);
-        c_.c_anc.ensure(4ull * nref_);
-        c_.c_g.ensure(4ull * nref_);
+        c_.c_anc.ensure(nref_);
+        c_.c_g.ensure(nref_);
         c_.c_dead.ensure(nref_);
         c_.ancless.ensure(nref_);
         c_.h_key.ensure(nsref);
         if (nconf_) {
           h2d(c_, c_.c_start.p, cstart_.data(), nconf_);
           h2d(c_, c_.c_key.p, ckey_.data(), nconf_);
-          h2d(c_, c_.c_fp.p, cfp_.data(), 4ull * nconf_);
-          h2d(c_, c_.c_anc.p, canc_.data(), 4ull * nconf_);
-          h2d(c_, c_.c_g.p, cg_.data(), 4ull * nconf_);
+          h2d(c_, c_.c_fp.p, cfp_.data(), nconf_);
+          h2d(c_, c_.c_anc.p, canc_.data(), nconf_);
+          h2d(c_, c_.c_g.p, cg_.data(), nconf_);
           HCK(hipMemsetAsync(c_.c_vis.p, 0, nconf_ * sizeof(uint64_t), c_.stream));
           HCK(hipMemsetAsync(c_.c_dead.p, 0, nconf_, c_.stream));
         }
@@ -1124,7 +1114,7 @@ class Resolver {
                         c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
-                        pre_sha_n_ ? c_.gsha.p : nullptr, pre_sha_n_, anchor_lo_, heads_for_epoch()};
+                        pre_sha_n_ ? c_.gsha.p : nullptr, pre_sha_n_};
         HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
@@ -2087,11 +2077,11 @@ class Resolver {
     uint32_t nk = 0;
     while (nk < nspec_ && ref_vis(nconf_ + nk) <= m) ++nk;  // vis grows with k
     if (!nk) return;
-    std::vector<uint64_t> fp(4ull * nk);
-    std::vector<uint32_t> g(4ull * nk), anc(4ull * nk);
-    d2h(c_, fp.data(), c_.c_fp.p + 4ull * nconf_, 4ull * nk);
-    d2h(c_, g.data(), c_.c_g.p + 4ull * nconf_, 4ull * nk);
-    d2h(c_, anc.data(), c_.c_anc.p + 4ull * nconf_, 4ull * nk);
+    std::vector<uint64_t> fp(nk);
+    std::vector<uint32_t> g(nk), anc(nk);
+    d2h(c_, fp.data(), c_.c_fp.p + nconf_, nk);
+    d2h(c_, g.data(), c_.c_g.p + nconf_, nk);
+    d2h(c_, anc.data(), c_.c_anc.p + nconf_, nk);
     sync(c_);
     const uint32_t base = nconf_;
     for (uint32_t k = 0; k < nk; ++k) {
@@ -2099,9 +2089,9 @@ class Resolver {
       if (dead_[ref]) continue;
       cstart_.push_back(ref_start(ref));
       ckey_.push_back(c_.h_key[k]);
-      cfp_.insert(cfp_.end(), fp.begin() + 4 * k, fp.begin() + 4 * k + 4);
-      cg_.insert(cg_.end(), g.begin() + 4 * k, g.begin() + 4 * k + 4);
-      canc_.insert(canc_.end(), anc.begin() + 4 * k, anc.begin() + 4 * k + 4);
+      cfp_.push_back(fp[k]);
+      cg_.push_back(g[k]);
+      canc_.push_back(anc[k]);
     }
     nconf_ = (uint32_t)cstart_.size();
   }
@@ -2127,32 +2117,6 @@ class Resolver {
     if (q >= pre_sha_n_ || ws + W_ > n_) return nullptr;
     return grid_sha() + 20 * q;
   }
-  // The first epoch's grid chunks [k W, (k + 1) W) (the stream's chunks unless
-  // matches move the grid): their anchors of the three residues the scan's
-  // pool does not hold come from their bytes, on the copy stream beside the
-  // scan (zc_heads_kernel), straight into the epoch's per-ref arrays
-  uint64_t heads_n_ = 0;
-  void pre_heads() {
-    heads_n_ = 0;
-    if (!indexable_ || n_ < 2ull * W_) return;
-    const uint64_t k = (n_ - 2ull * W_) / W_ + 1;  // the first epoch's nspec (r_e = 0)
-    if (k > 0x3FFFFFFFull) return;
-    c_.c_anc.ensure(4 * k);
-    c_.c_g.ensure(4 * k);
-    c_.c_fp.ensure(4 * k);
-    HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_in, 0));
-    HCK(launch_grid_heads(d_, n_, 0, (uint32_t)k, W_, anchor_lo_, c_.c_anc.p, c_.c_g.p, c_.c_fp.p, c_.copy_stream));
-    HCK(hipEventRecord(c_.ev_heads, c_.copy_stream));
-    heads_n_ = k;
-  }
-  // the epoch being set up is the first one: its grid chunks' heads are (being)
-  // computed -- the context's stream waits for them
-  bool heads_for_epoch() {
-    if (!heads_n_ || r_e_ != 0 || nconf_ != 0 || nspec_ > heads_n_) return false;
-    HCK(hipStreamWaitEvent(c_.stream, c_.ev_heads, 0));
-    return true;
-  }
-
   void pre_sha() {
     pre_sha_n_ = 0;
     gsha_ready_ = false;
@@ -2436,9 +2400,17 @@ size_t ctx_hbm_bytes(const zc_ctx& c) {
 
 }  // namespace
 
+#ifndef ZC_BUILD_ID
+#define ZC_BUILD_ID "unknown"
+#endif
+// kept in the binary as "zc-build-id:<digest>" so _build.py can read it
+// from the file without loading the library
+__attribute__((used)) const char kZcBuildTag[] = "zc-build-id:" ZC_BUILD_ID;
+
 extern "C" {
 
 int zc_abi_version(void) { return ZCHUNK_ABI_VERSION; }
+const char* zc_build_id(void) { return kZcBuildTag + 12; }
 
 int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags) {
   if (!out || chunk_max_size == 0) return ZC_ERR_ARG;
@@ -2459,7 +2431,6 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_sha, hipEventDisableTiming));
-    HCK(hipEventCreateWithFlags(&c->ev_heads, hipEventDisableTiming));
     HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
@@ -2486,7 +2457,6 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->ev_sha) (void)hipEventDestroy(c->ev_sha);
-    if (c->ev_heads) (void)hipEventDestroy(c->ev_heads);
     if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
