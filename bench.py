@@ -159,35 +159,37 @@ def cpu_baseline(sample_bytes, seed):
     return {"value": sample_bytes / dt / 2**30, "seconds": dt, "records": len(recs)}
 
 
-def pmc_traffic(n_bytes):
-    """HBM bytes per zc_scan launch from the committed rocprofv3 --pmc summary
-    (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE), if present."""
-    path = os.path.join(ROOT, "profiles", "scan_pmc.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if int(d.get("bytes", -1)) != int(n_bytes):
-            return None
-        return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-
-
-def rocprof_scan_ms():
-    """Average zc_scan_kernel duration (ms) from the newest committed rocprofv3
-    --kernel-trace --stats summary of the C2 bench (profiles/rNN_c2_kernel_stats.csv)."""
-    import csv
+def committed_profile(build_id):
+    """The newest committed profiles/rNN_scan_profile.json (tools/collect_profiles.py)
+    of THIS build of libzchunk.so, or None: a profile of other sources is never
+    quoted for this binary."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_c2_kernel_stats.csv")))
-    if not files:
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_scan_profile.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("build_id") == build_id:
+            d["path"] = os.path.relpath(path, ROOT)
+            return d
+    return None
+
+
+def pmc_traffic(prof, n_bytes):
+    """HBM bytes per zc_scan launch from the build's committed rocprofv3 --pmc
+    passes (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE)."""
+    if not prof or "pmc" not in prof or int(prof.get("bytes", -1)) != int(n_bytes):
+        return None
+    return prof["pmc"]["hbm_bytes_per_launch"]
+
+
+def rocprof_scan_ms(prof):
+    """Average zc_scan_kernel duration (ms) under rocprofv3 --kernel-trace --stats
+    of the C2 bench, from the build's committed summary."""
+    if not prof or "rocprof" not in prof:
         return None, None
-    with open(files[-1]) as f:
-        for r in csv.DictReader(f):
-            if r["Name"] == "zc_scan_kernel":
-                return float(r["AverageNs"]) * 1e-6, os.path.relpath(files[-1], ROOT)
-    return None, None
+    return prof["rocprof"]["avg_ms"], prof["rocprof"]["source"]
 
 
 def fill_edited(torch, buf, n, seed, local):
@@ -576,8 +578,11 @@ def run_rank(args):
                "per_process": [round(v, 5) for v in per]}
 
     if rank == 0:
+        from zbackup_amd import _lib
+        build_id = _lib.build_id()
+        prof = committed_profile(build_id)
         achieved = n / (scan_avg * 1e-3) / 1e9
-        rp_ms, rp_src = rocprof_scan_ms()
+        rp_ms, rp_src = rocprof_scan_ms(prof)
         out = {
             "metric": "rolling-hash chunking GiB/s (device-resident)",
             "value": round(value, 3),
@@ -599,8 +604,9 @@ def run_rank(args):
             "records_per_stream": nrec,
             "roofline": {"bound": "hbm", "kernel": "zc_scan_kernel", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(n), "bytes_per_launch": n,
+                         "traffic": pmc_traffic(prof, n), "bytes_per_launch": n,
                          "scan_ms_avg": round(scan_avg, 4)},
+            "build_id": build_id,
             "per_gpu_frac": [round(f, 4) for f in fracs],
             "stages": stage_dict(st),
         }
@@ -610,6 +616,10 @@ def run_rank(args):
                                           "achieved": round(n / (rp_ms * 1e-3) / 1e9, 1),
                                           "frac": round(n / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                           "source": rp_src}
+        if prof is None:
+            out["roofline"]["profile"] = f"no committed profiles/rNN_scan_profile.json of build {build_id}"
+        else:
+            out["roofline"]["profile"] = prof["path"]
         if "value_sha1" in extras:
             out["value_sha1"] = round(extras["value_sha1"], 3)
             out["sha1_ms_per_step"] = round(extras["sha1_ms_per_step"], 3)
