@@ -342,17 +342,21 @@ def stage_dict(st):
             "candidates": st["candidates"], "epochs": st["epochs"],
             "meta_ms": round(st["meta_ms"], 4), "probe_ms": round(st["probe_ms"], 4),
             "fscan_ms": round(st["fscan_ms"], 4), "walk_ms": round(st["walk_ms"], 4),
-            "finalize_ms": round(st["finalize_ms"], 4), "fbatch_ms": round(st["fbatch_ms"], 4)}
+            "finalize_ms": round(st["finalize_ms"], 4), "fbatch_ms": round(st["fbatch_ms"], 4),
+            "sha_wait_ms": round(st["sha_wait_ms"], 4), "sha_fill_ms": round(st["sha_fill_ms"], 4),
+            "hist_ms": round(st["hist_ms"], 4)}
 
 
-def feed_bench(n, seed, sha1, copy_threads=8):
+def feed_bench(n, seed, sha1, copy_threads=8, sha256=2):
     """tools/feedbench/feed_bench (built in-tree by build()): the zutils.cc read
     loop over the C++ binding, one process; the input copy is split over
-    copy_threads threads and reported apart from the engine's time."""
+    copy_threads threads and reported apart from the engine's time.  sha256:
+    the backup's whole-stream SHA-256 (zutils.cc:119), 1 inline after each read
+    as the reference does, 2 on a helper thread beside handleMoreData, 0 none."""
     exe = os.path.join(ROOT, "tools", "feedbench", "feed_bench")
     if not os.path.exists(exe):
         return None
-    out = subprocess.run([exe, str(W64), str(n), str(seed), "1" if sha1 else "0", str(copy_threads)],
+    out = subprocess.run([exe, str(W64), str(n), str(seed), "1" if sha1 else "0", str(copy_threads), str(sha256)],
                          capture_output=True, text=True, timeout=600)
     if out.returncode != 0:
         return {"error": out.stderr.strip()[-300:]}
@@ -364,6 +368,8 @@ def feed_bench(n, seed, sha1, copy_threads=8):
             "writer_add_s": d["writer_add_s"], "engine_and_adapter_s": eng, "shrink_s": d["shrink_s"],
             "shrink_iterations": d["shrink_iterations"], "writer_chunks": d["writer_chunks"],
             "bundles": d["bundles"], "window_bytes": d["window_bytes"], "pieces": d["pieces"],
+            "sha256": {0: "none", 1: "inline after each read (zutils.cc:119)",
+                       2: "helper thread beside handleMoreData"}[sha256], "sha256_s": d["sha256_s"],
             "path": "zutils.cc read loop over integration/gpu_backup_creator.hh: memcpy into getInputBuffer "
                     f"({copy_threads} threads, standing for fread), handleMoreData through the bounded window, "
                     "records drained as cut (zc_take_records, zc_read_stream -> Writer::add into 2 MiB bundle "
@@ -556,10 +562,14 @@ def run_rank(args):
         # payload, Message::serialize of every record), finish, getBackupData, the
         # shrink passes; rolling-hash ids and complete ChunkIds
         if args.config == "c2":
-            for sha1 in (False, True):
-                fb = feed_bench(n, seed, sha1)
+            # feed: the engine's part alone (no whole-stream SHA-256); feed_sha1:
+            # the reference loop whole -- complete ChunkIds and the backup's
+            # SHA-256 of every piece, on a helper thread (and inline, as
+            # zutils.cc:119 runs it, in feed_sha1_inline_sha256)
+            for key, sha1, s256 in (("feed", False, 0), ("feed_sha1", True, 2), ("feed_sha1_inline_sha256", True, 1)):
+                fb = feed_bench(n, seed, sha1, sha256=s256)
                 if fb:
-                    extras["feed_sha1" if sha1 else "feed"] = fb
+                    extras[key] = fb
         if args.config == "c2" and args.lzo:
             extras["bundle_lzo"] = bundle_leg(torch, buf, n, recs, world, local, rank == 0)
 
@@ -635,7 +645,7 @@ def run_rank(args):
                 out[key] = e
         if "incremental" in extras:
             out["incremental_sha1"] = extras["incremental"]
-        for key in ("feed", "feed_sha1"):
+        for key in ("feed", "feed_sha1", "feed_sha1_inline_sha256"):
             if key in extras:
                 out[key] = extras[key]
         if "bundle_lzo" in extras:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ZCHUNK_ABI_VERSION 2
+#define ZCHUNK_ABI_VERSION 3
 
 enum zc_status {
   ZC_OK = 0,
@@ -104,6 +104,10 @@ typedef struct {
   uint64_t hbm_bytes;    /* device memory the context holds now */
   uint64_t segments;     /* window segments resolved during the feed */
   uint64_t hist_entries; /* historic index entries (chunks whose bytes have left HBM) */
+  /* parts of finalize_ms (ZC_FLAG_SHA1): */
+  double sha_wait_ms;    /* blocked on the grid chunks' SHA-1 and its copy to the host */
+  double sha_fill_ms;    /* SHA-1 prefixes into the records (and the new chunks' list) */
+  double hist_ms;        /* the stream's new chunks joining the context's index */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;

@@ -118,6 +118,28 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
+# SHA-1 ids with the whole stream in one scan launch and at least one grid
+# chunk per scan lane (512 lanes per 2 MiB tile, one workgroup per CU up to 256):
+# the scan's lanes hash the grid chunks themselves (launch_scan_sha).  Cases:
+# a chunk ending in every round (W = 128), lanes with one chunk more than
+# others and more blocks than the rounds hold (the tail loop), W not a power of
+# two, a 3-byte partial last chunk, duplicates moving the grid, and 260 tiles
+# (workgroups with one and with two tiles)
+@pytest.mark.parametrize("W,spec", [
+    (128, "R31:50000000,C7:3000000,R32:333"),
+    (1024, "R33:40000000,Z:2000000,C123:5000000,R34:77777"),
+    (2944, "R35:50331648"),
+    (4096, "R36:50343939"),
+    (1024, "R37:545259520,R38:4321"),
+])
+def test_fused_scan_sha1_vs_oracle(torch_cuda, W, spec):
+    data = oracle.gen(spec)
+    ntiles = data.size // (2 << 20)
+    assert data.size // W >= min(ntiles, 256) * 512  # fusable on a 256-CU MI355X
+    want = oracle.chunk(data, W)
+    assert _run_device(torch_cuda, data, W) == want
+
+
 # tiny chunk sizes: below the anchor offset (every ref anchorless: the exact
 # screen alone) and below the staged screen's 32-byte minimum
 @pytest.mark.parametrize("W", [1, 2, 7, 16, 31, 32, 33, 63, 64, 65])

@@ -7,13 +7,20 @@
 // zc_read_stream into Writer::add, which appends them to a 2 MiB bundle
 // payload; every record through Message::serialize), finish, getBackupData,
 // then the iterative shrink passes (zutils.cc:137-166) on the same index.
+// The backup's whole-stream SHA-256 (BackupInfo.sha256, zutils.cc:94,119,134)
+// is kept too: sha256 = 1 adds every piece inline after the read, as the
+// reference loop does (a serial chain: the loop can run no faster than it);
+// 2 hashes piece i on a helper thread while handleMoreData(i) runs, joined
+// before the next getInputBuffer (the piece's bytes are overwritten then);
+// 0 leaves it out.
 //
-//   feed_bench W bytes seed sha1(0|1) copy_threads
+//   feed_bench W bytes seed sha1(0|1) copy_threads [sha256(0|1|2)]
 // prints one JSON object: seconds of the whole loop and of its parts
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <chrono>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -57,10 +64,11 @@ void copy_mt(void* dst, const void* src, size_t n, unsigned threads) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc != 6) {
-    fprintf(stderr, "usage: %s W bytes seed sha1 copy_threads\n", argv[0]);
+  if (argc != 6 && argc != 7) {
+    fprintf(stderr, "usage: %s W bytes seed sha1 copy_threads [sha256]\n", argv[0]);
     return 2;
   }
+  const int sha256_mode = argc == 7 ? atoi(argv[6]) : 0;
   const uint32_t W = (uint32_t)strtoul(argv[1], 0, 10);
   const uint64_t n = strtoull(argv[2], 0, 0), seed = strtoull(argv[3], 0, 0);
   const bool sha1 = atoi(argv[4]) != 0;
@@ -75,12 +83,20 @@ int main(int argc, char** argv) {
   ChunkStorage::Writer writer;
   try {
     GpuChunkIndex gpuIndex(config, chunkIndex, 0, sha1 ? ZC_FLAG_SHA1 : 0);
-    double copy_s = 0;
+    double copy_s = 0, sha256_s = 0;
     size_t pieces = 0;
+    zc_sha256* sha256 = nullptr;
+    if (sha256_mode && zc_sha256_create(&sha256) != ZC_OK) throw std::runtime_error("zc_sha256_create");
+    std::thread hasher;
     const auto t0 = Clock::now();
     GpuBackupCreator backupCreator(gpuIndex, writer);
     uint64_t pos = 0;
     for (;;) {
+      if (hasher.joinable()) {  // the previous piece's bytes are hashed before they are overwritten
+        const auto tj = Clock::now();
+        hasher.join();
+        sha256_s += since(tj);
+      }
       size_t toRead = backupCreator.getInputBufferSize();
       void* inputBuffer = backupCreator.getInputBuffer();
       const size_t rd = (size_t)std::min<uint64_t>(toRead, n - pos);
@@ -90,9 +106,27 @@ int main(int argc, char** argv) {
       copy_s += since(tc);
       pos += rd;
       ++pieces;
+      if (sha256_mode == 1) {  // zutils.cc:119
+        const auto th = Clock::now();
+        zc_sha256_add(sha256, inputBuffer, rd);
+        sha256_s += since(th);
+      } else if (sha256_mode == 2) {
+        hasher = std::thread([=] { zc_sha256_add(sha256, inputBuffer, rd); });
+      }
       backupCreator.handleMoreData((unsigned)rd);
     }
     backupCreator.finish();
+    std::string sha256_hex;
+    if (sha256) {
+      uint8_t dg[32];
+      zc_sha256_finish(sha256, dg);
+      zc_sha256_destroy(sha256);
+      char hx[3];
+      for (uint8_t b : dg) {
+        snprintf(hx, sizeof hx, "%02x", b);
+        sha256_hex += hx;
+      }
+    }
     std::string serialized;
     backupCreator.getBackupData(serialized);
     const double loop_s = since(t0);
@@ -126,10 +160,11 @@ int main(int argc, char** argv) {
     printf("{\"bytes\": %llu, \"W\": %u, \"sha1\": %d, \"copy_threads\": %u, \"pieces\": %zu, \"loop_s\": %.6f, "
            "\"copy_s\": %.6f, \"writer_add_s\": %.6f, \"engine_and_adapter_s\": %.6f, \"shrink_s\": %.6f, "
            "\"shrink_iterations\": %u, \"writer_chunks\": %zu, \"writer_bytes\": %zu, \"bundles\": %zu, "
-           "\"backup_data_bytes\": %zu, \"window_bytes\": %llu}\n",
+           "\"backup_data_bytes\": %zu, \"window_bytes\": %llu, \"sha256_mode\": %d, \"sha256_s\": %.6f, "
+           "\"sha256\": \"%s\"}\n",
            (unsigned long long)n, W, sha1 ? 1 : 0, threads, pieces, loop_s, copy_s, writer.seconds,
-           loop_s - copy_s - writer.seconds, shrink_s, iterations, writer.chunks, writer.bytes, writer.bundles + 1,
-           serialized.size(), (unsigned long long)stats.window_bytes);
+           loop_s - copy_s - writer.seconds - sha256_s, shrink_s, iterations, writer.chunks, writer.bytes, writer.bundles + 1,
+           serialized.size(), (unsigned long long)stats.window_bytes, sha256_mode, sha256_s, sha256_hex.c_str());
   } catch (const std::exception& e) {
     fprintf(stderr, "feed_bench: %s\n", e.what());
     return 1;

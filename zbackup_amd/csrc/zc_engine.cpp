@@ -30,6 +30,8 @@
 //     the bytes it covers, so a stream with many grid shifts stays linear.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 #include <emmintrin.h>
@@ -270,6 +272,24 @@ class HostPool {
 // 40-byte records are five 16-byte words, streamed past the caches (no
 // read-for-ownership of the lines they overwrite)
 constexpr uint64_t kParallelRecordsMin = 32768;
+
+// diagnostics (ZC_TRACE=1): host phase times of the stream end, to stderr
+struct Trace {
+  bool on = getenv("ZC_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    char b[64];
+    snprintf(b, sizeof b, " %s=%.3f", what, std::chrono::duration<double, std::milli>(n - t).count());
+    line += b;
+    t = n;
+  }
+  ~Trace() {
+    if (on && !line.empty()) fprintf(stderr, "zc_trace:%s\n", line.c_str());
+  }
+};
 void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uint32_t W, uint32_t kind,
                        const uint64_t* key) {
   auto fill = [&](size_t a, size_t b) {
@@ -312,8 +332,12 @@ struct zc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
   hipStream_t sha_stream = nullptr;   // SHA-1 of the grid chunks, beside the scan (ZC_FLAG_SHA1)
+  hipStream_t sha_stream2 = nullptr;  // the early part of a listed grid SHA-1
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   hipEvent_t ev_sha = nullptr;  // the grid chunks' SHA-1 (sha_stream) are complete
+  hipEvent_t ev_lead = nullptr;  // the first epoch's class leads (and SHA-1 list) are complete
+  hipEvent_t ev_list = nullptr;  // ... and the list is on the host
+  hipEvent_t ev_sha2 = nullptr;  // the early part of the listed SHA-1 is complete
   std::string err;
 
   // host feed
@@ -385,6 +409,9 @@ struct zc_ctx {
   DevBuf<unsigned long long> counters;
   DevBuf<uint8_t> gsha;  // SHA-1 of the first epoch's grid chunks (ZC_FLAG_SHA1)
   HostBuf<uint8_t> h_gsha;  // ... copied back on the SHA-1 stream right behind the kernel
+  DevBuf<uint32_t> sha_list;  // the grid chunks the class leads list for the SHA-1
+  DevBuf<unsigned long long> sha_cnt;  // their count, copied out of the counters (later epochs clear those)
+  HostBuf<uint32_t> h_shalist;
   HostBuf<uint64_t> h_hmkey;  // pinned staging of the keys and anchors of new historic entries
   HostBuf<uint32_t> h_hmanc;
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
@@ -558,6 +585,7 @@ class Resolver {
   }
   void drain() {
     (void)hipStreamSynchronize(c_.sha_stream);
+    (void)hipStreamSynchronize(c_.sha_stream2);
     (void)hipStreamSynchronize(c_.copy_stream);
     (void)hipStreamSynchronize(c_.stream);
   }
@@ -582,6 +610,10 @@ class Resolver {
     hist0_ = c_.nhist;
     statics0_ = c_.statics.size();
     r_ = s_ = x_resume_ = hspan_ = 0;
+    fused_sha_ = sha_deferred_ = false;
+    sha_classes_ = sha_listed_ = sha_counted_ = false;
+    shal_n_ = 0;
+    sha_src_.clear();
     scan_setup();
   }
   // bytes [0, n) of the stream are (being) copied to the device, in order on
@@ -598,9 +630,20 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
-      // with chunk ids of a whole-stream run the grid SHA-1 shares the CUs
-      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
-                            c_.stream, !windowed_ && (c_.flags & ZC_FLAG_SHA1)));
+      const bool sha = !windowed_ && (c_.flags & ZC_FLAG_SHA1) && indexable_ && sha_mode() == 1;
+      if (!windowed_ && (c_.flags & ZC_FLAG_SHA1) && indexable_ && sha_mode() == 0 && tiles_done_ == 0 && t1 == n_ / ZC_STILE && sha_fusable(n_, W_, t1)) {
+        // the whole stream in one launch: the scan's lanes hash the grid
+        // chunks too (pre_sha() adds a partial last chunk)
+        const uint64_t k = (n_ + W_ - 1) / W_;
+        c_.gsha.ensure(k * 20);
+        HCK(launch_scan_sha(d_, n_, t1, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
+                            ShaFuse{c_.gsha.p, n_ / W_, W_}, c_.stream));
+        fused_sha_ = true;
+      } else {
+        // with chunk ids of a whole-stream run the grid SHA-1 shares the CUs
+        HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(),
+                              c_.counters.p, c_.stream, sha));
+      }
       tiles_done_ = t1;
     }
   }
@@ -728,7 +771,7 @@ class Resolver {
   // hist_add_sha completes the entries once their SHA-1 prefixes are known.
   struct HistPending {
     uint32_t e0 = 0, k = 0;
-    std::vector<uint32_t> anc;
+    const uint32_t* anc = nullptr;  // the entries' first anchors (host), complete after a sync
   };
   HistPending hist_add_meta(const std::vector<uint64_t>& starts) {
     HistPending hp;
@@ -739,69 +782,97 @@ class Resolver {
     c_.hanc.grow_keep(e0 + k, e0, c_.stream);
     c_.hg.grow_keep(e0 + k, e0, c_.stream);
     c_.hfp.grow_keep(e0 + k, e0, c_.stream);
-    c_.hm_key.ensure(k);
-    // chunks that are refs of the current epoch take the metadata it computed
-    // (its grid chunks, its confirmed refs); the rest is computed from the bytes
-    std::vector<uint32_t> gsrc, gdst;
-    std::vector<uint64_t> rest;
-    std::vector<uint32_t> rdst;
-    for (uint32_t t = 0; t < k; ++t) {
-      const int64_t ref = epoch_ref_at(starts[t]);
-      if (ref >= 0) {
-        gsrc.push_back((uint32_t)ref);
-        gdst.push_back(t);
-      } else {
-        rest.push_back(starts[t]);
-        rdst.push_back(t);
-      }
-    }
-    if (!gsrc.empty()) {
-      const uint32_t m = (uint32_t)gsrc.size();
-      c_.gidx.ensure(2ull * m);
-      h2d(c_, c_.gidx.p, gsrc.data(), m);
-      h2d(c_, c_.gidx.p + m, gdst.data(), m);
-      HCK(launch_ref_gather(c_.gidx.p, c_.gidx.p + m, m, c_.c_key.p, c_.c_anc.p, c_.c_g.p, c_.c_fp.p, c_.hm_key.p,
-                            c_.hanc.p + e0, c_.hg.p + e0, c_.hfp.p + e0, c_.stream));
-    }
-    if (!rest.empty()) {
-      // computed into the staging slots after the gathered ones, then moved
-      const uint32_t m = (uint32_t)rest.size();
-      c_.hm_anc.ensure(m);
-      c_.hm_g.ensure(m);
-      c_.hm_fp.ensure(m);
-      c_.hm_rkey.ensure(m);
-      h2d(c_, c_.va.p, rest.data(), m);
-      HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, m, W_, pow257(W_), c_.hm_rkey.p, c_.hm_anc.p, c_.hm_g.p,
-                          c_.hm_fp.p, c_.stream));
-      std::vector<uint32_t> src(m);
-      for (uint32_t t = 0; t < m; ++t) src[t] = t;
-      c_.gidx.ensure(2ull * m);
-      h2d(c_, c_.gidx.p, src.data(), m);
-      h2d(c_, c_.gidx.p + m, rdst.data(), m);
-      HCK(launch_ref_gather(c_.gidx.p, c_.gidx.p + m, m, c_.hm_rkey.p, c_.hm_anc.p, c_.hm_g.p, c_.hm_fp.p,
-                            c_.hm_key.p, c_.hanc.p + e0, c_.hg.p + e0, c_.hfp.p + e0, c_.stream));
-    }
-    c_.h_hmkey.ensure(k);
     c_.h_hmanc.ensure(k);
-    d2h(c_, c_.h_hmkey.p, c_.hm_key.p, k);
-    d2h(c_, c_.h_hmanc.p, c_.hanc.p + e0, k);
-    sync(c_);
+    // a leading run of consecutive grid chunks of the epoch whose metadata the
+    // device arrays hold (a whole stream's new chunks, but for the last one or
+    // two that finish() cuts) is copied as it is, its keys from the host's
+    // copy of the epoch's; the rest is gathered by index lists
+    uint32_t run = 0;
+    const int64_t ref0 = epoch_ref_at(starts[0]);
+    if (ref0 >= (int64_t)dev_nconf_) {
+      const uint64_t lim = std::min<uint64_t>(k, (uint64_t)dev_nconf_ + dev_nspec_ - (uint64_t)ref0);
+      while (run < lim && starts[run] == starts[0] + (uint64_t)run * W_) ++run;
+    }
     c_.hkey.resize((size_t)e0 + k);
-    memcpy(c_.hkey.data() + e0, c_.h_hmkey.p, k * sizeof(uint64_t));
-    hp.anc.assign(c_.h_hmanc.p, c_.h_hmanc.p + k);
+    if (run) {
+      const uint32_t r0 = (uint32_t)ref0;
+      HCK(hipMemcpyAsync(c_.hanc.p + e0, c_.c_anc.p + r0, run * sizeof(uint32_t), hipMemcpyDeviceToDevice, c_.stream));
+      HCK(hipMemcpyAsync(c_.hg.p + e0, c_.c_g.p + r0, run * sizeof(uint32_t), hipMemcpyDeviceToDevice, c_.stream));
+      HCK(hipMemcpyAsync(c_.hfp.p + e0, c_.c_fp.p + r0, run * sizeof(uint64_t), hipMemcpyDeviceToDevice, c_.stream));
+      memcpy(c_.hkey.data() + e0, c_.h_key.p + (r0 - dev_nconf_), run * sizeof(uint64_t));
+    }
+    tr_.mark("hm_run");
+    if (run < k) {
+      const uint32_t kr = k - run;  // entries e0 + run + t, t < kr
+      c_.hm_key.ensure(kr);
+      // chunks that are refs of the current epoch take the metadata it
+      // computed (its grid chunks, its confirmed refs); the rest is computed
+      // from the bytes
+      std::vector<uint32_t> gsrc, gdst;
+      std::vector<uint64_t> rest;
+      std::vector<uint32_t> rdst;
+      for (uint32_t t = 0; t < kr; ++t) {
+        const int64_t ref = epoch_ref_at(starts[run + t]);
+        if (ref >= 0) {
+          gsrc.push_back((uint32_t)ref);
+          gdst.push_back(t);
+        } else {
+          rest.push_back(starts[run + t]);
+          rdst.push_back(t);
+        }
+      }
+      const uint32_t eb = e0 + run;
+      c_.gidx.ensure(2ull * kr);  // both lists' index pairs, allocated before either launch
+      if (!gsrc.empty()) {
+        const uint32_t m = (uint32_t)gsrc.size();
+        h2d(c_, c_.gidx.p, gsrc.data(), m);
+        h2d(c_, c_.gidx.p + m, gdst.data(), m);
+        HCK(launch_ref_gather(c_.gidx.p, c_.gidx.p + m, m, c_.c_key.p, c_.c_anc.p, c_.c_g.p, c_.c_fp.p, c_.hm_key.p,
+                              c_.hanc.p + eb, c_.hg.p + eb, c_.hfp.p + eb, c_.stream));
+      }
+      if (!rest.empty()) {
+        // computed into the staging slots after the gathered ones, then moved
+        const uint32_t m = (uint32_t)rest.size();
+        c_.hm_anc.ensure(m);
+        c_.hm_g.ensure(m);
+        c_.hm_fp.ensure(m);
+        c_.hm_rkey.ensure(m);
+        h2d(c_, c_.va.p, rest.data(), m);
+        HCK(launch_ref_meta(d_, blk_v(), av(), c_.va.p, m, W_, pow257(W_), c_.hm_rkey.p, c_.hm_anc.p, c_.hm_g.p,
+                            c_.hm_fp.p, c_.stream));
+        std::vector<uint32_t> src(m);
+        for (uint32_t t = 0; t < m; ++t) src[t] = t;
+        uint32_t* gi = c_.gidx.p + 2ull * gsrc.size();
+        h2d(c_, gi, src.data(), m);
+        h2d(c_, gi + m, rdst.data(), m);
+        HCK(launch_ref_gather(gi, gi + m, m, c_.hm_rkey.p, c_.hm_anc.p, c_.hm_g.p, c_.hm_fp.p, c_.hm_key.p,
+                              c_.hanc.p + eb, c_.hg.p + eb, c_.hfp.p + eb, c_.stream));
+      }
+      c_.h_hmkey.ensure(kr);
+      d2h(c_, c_.h_hmkey.p, c_.hm_key.p, kr);
+      sync(c_);
+      memcpy(c_.hkey.data() + eb, c_.h_hmkey.p, kr * sizeof(uint64_t));
+    }
+    tr_.mark("hm_rest");
+    // the entries' anchors, for hist_add_sha (it synchronises first)
+    d2h(c_, c_.h_hmanc.p, c_.hanc.p + e0, k);
+    hp.anc = c_.h_hmanc.p;
     c_.nhist = e0 + k;
     hist_table(c_, e0);
+    tr_.mark("hm_table");
     hp.e0 = e0;
     hp.k = k;
     return hp;
   }
   // sha16: the entries' SHA-1 prefixes, 16 bytes each; entries without an
   // anchor also join the by-value set of the exact screen
+  // (sha16 null: already in place in c_.hsha)
   void hist_add_sha(const HistPending& hp, const uint8_t* sha16) {
     if (!hp.k) return;
+    sync(c_);  // hp.anc has landed
     c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
     uint8_t* hs = c_.hsha.data() + 16 * (size_t)hp.e0;
-    memcpy(hs, sha16, 16 * (size_t)hp.k);
+    if (sha16) memcpy(hs, sha16, 16 * (size_t)hp.k);
     for (uint32_t i = 0; i < hp.k; ++i)
       if (hp.anc[i] == ZC_NO_ANCHOR) add_static_once(c_, c_.hkey[hp.e0 + i], hs + 16 * (size_t)i, 0);
   }
@@ -1110,12 +1181,19 @@ class Resolver {
         c_.ckeys.ensure(1u << tbits);
         c_.c_cls.ensure(nref_);
         c_.cpairs.ensure(nref_);
+        // classes first (sha_classes_): the stream's first epoch lists its
+        // leading grid chunks for the SHA-1, launched right behind the leads
+        const bool list_sha = sha_classes_ && !sha_listed_ && r_e_ == 0 && nconf_ == 0;
+        if (list_sha) c_.sha_list.ensure(std::max<uint32_t>(nsref, 1));
         ix = EpochIndex{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
                         c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
-                        pre_sha_n_ ? c_.gsha.p : nullptr, pre_sha_n_};
-        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
+                        pre_sha_n_ && !sha_classes_ && sha_mode() != 2 ? c_.gsha.p : nullptr, pre_sha_n_,
+                        list_sha ? c_.sha_list.p : nullptr, n_ / W_};
+        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream,
+                               list_sha ? c_.ev_lead : nullptr));
+        if (list_sha) sha_launch_listed(nsref);
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
         dev_nspec_ = nsref;
@@ -1132,6 +1210,7 @@ class Resolver {
         HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
                          c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
                          c_.stream));
+      sha_launch_deferred();
       HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
       if (nsref)
         HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1142,8 +1221,17 @@ class Resolver {
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
       HCK(hipStreamSynchronize(c_.copy_stream));
+      if (sha_listed_ && !sha_counted_) {
+        shal_n_ = c_.h_cnt[CNT_SHAL];
+        sha_counted_ = true;
+      }
       if (scan_check()) {  // the pool changed under this epoch: queue it again
         c_.stats.epochs--;
+        // (the re-run rewrites the class arrays the listed SHA-1 may still read)
+        if (sha_listed_) {
+          HCK(hipStreamSynchronize(c_.sha_stream2));
+          HCK(hipStreamSynchronize(c_.sha_stream));
+        }
         return true;
       }
       if (nref_ && c_.h_cnt[CNT_SPAIRS]) {
@@ -1165,6 +1253,7 @@ class Resolver {
       ncand = anchors ? c_.h_cnt[CNT_CAND] : 0;
       nancless = nref_ ? c_.h_cnt[CNT_ANCLESS] : 0;
       if (nref_ && c_.h_cnt[CNT_CLASS]) load_classes();
+      if (sha_listed_ && sha_src_.empty()) sha_sources(nsref);
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
@@ -2105,7 +2194,8 @@ class Resolver {
   bool gsha_ready_ = false;
   const uint8_t* grid_sha() {
     if (!gsha_ready_) {
-      if (pre_sha_n_) HCK(hipStreamSynchronize(c_.sha_stream));  // the kernel and the copy behind it
+      sha_launch_deferred();
+      if (pre_sha_n_) HCK(hipStreamSynchronize(c_.sha_stream));  // (ordered after sha_stream2's part)  // the kernel and the copy behind it
       gsha_ready_ = true;
     }
     return c_.h_gsha.p;
@@ -2115,7 +2205,93 @@ class Resolver {
     if (!pre_sha_n_ || ws % W_) return nullptr;
     const uint64_t q = ws / W_;
     if (q >= pre_sha_n_ || ws + W_ > n_) return nullptr;
-    return grid_sha() + 20 * q;
+    const uint8_t* g = grid_sha();  // (classes first: the sources are known once the SHA-1 is queued)
+    const uint32_t src = sha_slot(q);
+    return src == kNone ? nullptr : g + 20ull * src;
+  }
+  bool fused_sha_ = false;  // the scan launch hashes the whole grid chunks (launch_scan_sha)
+  bool sha_deferred_ = false;
+  // Classes first: the grid SHA-1 hashes only the chunks that lead their key
+  // in the stream's first epoch (and the grid chunks that are no refs); a
+  // chunk whose bytes the epoch verified equal to its leader's takes the
+  // leader's digest (sha_src_), one whose check failed is hashed with the
+  // records that are no grid chunks.  Duplicated content is hashed once.
+  bool sha_classes_ = false, sha_listed_ = false, sha_counted_ = false;
+  uint64_t shal_n_ = 0;
+  uint32_t sha_nsref_ = 0;
+  std::vector<uint32_t> sha_src_;  // grid chunk -> the chunk whose digest is its own (kNone: hash it)
+  // The listed SHA-1 in two parts.  Early, right behind the class leads and
+  // beside the rest of the epoch's batch: the grid chunks after the refs and
+  // the first kEarlySha listed ones -- at most a few waves, too few to hold
+  // the SIMDs the batch's latency-bound kernels need (a full SHA-1 grid beside
+  // them stretched the probe from 0.07 to 3.9 ms), and what is left when
+  // duplicated content lists few chunks (all-zero data lists one, whose 64 KiB
+  // chain then hashes while the byte checks run).  Late, behind the batch
+  // (sha_launch_deferred): the rest of the list.
+  static constexpr uint32_t kEarlySha = 1024;
+  void sha_launch_listed(uint32_t nsref) {
+    sha_listed_ = true;
+    sha_nsref_ = nsref;
+    const uint64_t k = pre_sha_n_;
+    c_.h_shalist.ensure(std::max<uint32_t>(nsref, 1));
+    c_.sha_cnt.ensure(1);
+    HCK(hipStreamWaitEvent(c_.sha_stream2, c_.ev_lead, 0));
+    HCK(hipMemcpyAsync(c_.sha_cnt.p, c_.counters.p + CNT_SHAL, sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                       c_.sha_stream2));
+    if (nsref) {
+      HCK(hipMemcpyAsync(c_.h_shalist.p, c_.sha_list.p, nsref * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         c_.sha_stream2));
+      HCK(hipEventRecord(c_.ev_list, c_.sha_stream2));
+    }
+    HCK(launch_sha1_list(d_, n_, W_, c_.sha_list.p, c_.sha_cnt.p, 0, std::min(nsref, kEarlySha), nsref,
+                         (uint32_t)(k - nsref), c_.gsha.p, c_.sha_stream2));
+    HCK(hipEventRecord(c_.ev_sha2, c_.sha_stream2));
+    sha_deferred_ = nsref > kEarlySha;  // the rest behind the batch
+    if (!sha_deferred_) {
+      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha2, 0));
+      HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+      HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
+    }
+  }
+  // after the first epoch's classes are known (cls_, empty: no class has
+  // members): the digest source of every grid chunk
+  void sha_sources(uint32_t nsref) {
+    const uint64_t k = pre_sha_n_;
+    sha_src_.assign(k, kNone);
+    if (nsref) HCK(hipEventSynchronize(c_.ev_list));
+    for (uint64_t t = 0; t < shal_n_; ++t) sha_src_[c_.h_shalist.p[t]] = c_.h_shalist.p[t];
+    for (uint64_t q = nsref; q < k; ++q) sha_src_[q] = (uint32_t)q;
+    if (!cls_.empty())
+      for (uint32_t q = 0; q < nsref && q < cls_.size(); ++q)
+        if (sha_src_[q] == kNone && cls_[q] != q && sha_src_[cls_[q]] == cls_[q]) sha_src_[q] = cls_[q];
+  }
+  // the chunk whose digest slot holds grid chunk q's SHA-1, or kNone
+  uint32_t sha_slot(uint64_t q) const {
+    if (!sha_classes_) return (uint32_t)q;
+    return q < sha_src_.size() ? sha_src_[q] : kNone;
+  }
+  // experiment: ZC_SHA_MODE 0 fused (default), 1 a SHA-1 kernel beside the scan,
+  // 2 a SHA-1 kernel behind the first epoch's batch
+  int sha_mode() const {
+    const char* e = getenv("ZC_SHA_MODE");
+    return e ? atoi(e) : 0;
+  }
+  void sha_launch_deferred() {
+    if (!sha_deferred_) return;
+    sha_deferred_ = false;
+    const uint64_t k = pre_sha_n_;
+    HCK(hipEventRecord(c_.ev_sha, c_.stream));
+    HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
+    if (sha_listed_) {
+      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_list, 0));  // the count copied out (sha_stream2)
+      HCK(launch_sha1_list(d_, n_, W_, c_.sha_list.p, c_.sha_cnt.p, kEarlySha, sha_nsref_, 0, 0, c_.gsha.p,
+                           c_.sha_stream));
+      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha2, 0));
+    } else {
+      HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+    }
+    HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+    HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
   }
   void pre_sha() {
     pre_sha_n_ = 0;
@@ -2125,9 +2301,31 @@ class Resolver {
     if (k > 0xFFFFFFFFull) return;
     c_.gsha.ensure(k * 20);
     c_.h_gsha.ensure(k * 20);
-    HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
-    HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
-    HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+    if (fused_sha_) {
+      // done by the scan, on the context's stream; a partial last chunk here
+      if (n_ % W_) HCK(launch_sha1_one(d_, n_ / W_ * W_, (uint32_t)(n_ % W_), (uint32_t)(n_ / W_), c_.gsha.p,
+                                       c_.stream));
+      HCK(hipEventRecord(c_.ev_sha, c_.stream));
+      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
+    } else if (sha_mode() == 2) {
+      sha_deferred_ = true;  // launched behind the first epoch's batch (sha_launch_deferred)
+      pre_sha_n_ = k;
+      return;
+    } else if (sha_mode() == 5 && W_ % 16 == 0) {
+      sha_classes_ = true;  // launched behind the first epoch's class leads (sha_launch_listed)
+      pre_sha_n_ = k;
+      return;
+    } else if (sha_mode() == 1) {
+      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
+      HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+      HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+    } else {
+      // behind the scan (not beside it), ahead of the epoch's batch
+      HCK(hipEventRecord(c_.ev_sha, c_.stream));
+      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
+      HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+      HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+    }
     HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
     pre_sha_n_ = k;
   }
@@ -2137,6 +2335,7 @@ class Resolver {
   // and (ZC_FLAG_SHA1) every chunk record its SHA-1 prefix.
   std::vector<uint64_t> fresh_;  // NEW W-byte chunks of the stream still resident: offset,
   std::vector<uint8_t> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
+  Trace tr_;
   // stream_end: the stream's end (run_final): with ZC_FLAG_SHA1 its new W-byte
   // chunks join the context's index here, their device metadata queued before
   // the wait for the grid SHA-1, so that wait ends the call with little after it
@@ -2147,6 +2346,7 @@ class Resolver {
       Clock::time_point t;
       ~Done() { st.finalize_ms += ms_since(t); }
     } done{c_.stats, t0};
+    if (stream_end) tr_.mark("to_finalize");
     std::vector<uint64_t> a, b;
     std::vector<size_t> rest;
     for (size_t i = 0; i < need_digest_.size(); ++i) {
@@ -2182,42 +2382,64 @@ class Resolver {
     std::vector<uint64_t> sa;
     std::vector<uint32_t> sl;
     std::vector<size_t> idx;
+    std::vector<uint64_t> gq;    // grid-chunk records: record index << 32 | chunk (both < 2^32)
+    std::vector<uint32_t> frec;  // record (from r0) of each new fresh_ entry
     const size_t f0 = fresh_.size();
+    gq.reserve(r1 - r0);
     for (size_t i = r0; i < r1; ++i) {
       const zc_record& r = c_.recs[i];
       if (r.kind == ZC_BYTES) continue;
-      if (r.kind == ZC_CHUNK_NEW && r.size == W_) fresh_.push_back(r.offset);
-      if (grid_q(r) != kInf) continue;
+      if (r.kind == ZC_CHUNK_NEW && r.size == W_) {
+        fresh_.push_back(r.offset);
+        frec.push_back((uint32_t)(i - r0));
+      }
+      const uint64_t q = grid_q(r);
+      const uint32_t src = q != kInf ? sha_slot(q) : kNone;
+      if (src != kNone) {
+        gq.push_back((uint64_t)(i - r0) << 32 | src);
+        continue;
+      }
       sa.push_back(r.offset);
       sl.push_back(r.size);
       idx.push_back(i);
     }
+    tr_.mark("rec_loop");
     std::vector<uint8_t> sh = sha1s(sa, sl);
+    tr_.mark("sha1s");
     HistPending hp;
+    auto th = Clock::now();
     if (stream_end) hp = hist_add_meta(fresh_);
+    tr_.mark("hist_meta");
+    c_.stats.hist_ms += ms_since(th);
+    auto tw = Clock::now();
     const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;  // waits for the side stream
-    auto fill = [&](size_t a0, size_t a1) {
-      for (size_t i = r0 + a0; i < r0 + a1; ++i) {
-        zc_record& r = c_.recs[i];
-        if (r.kind == ZC_BYTES) continue;
-        const uint64_t q = grid_q(r);
-        if (q != kInf) memcpy(r.sha1, &gsha[q * 20], 16);
-      }
-    };
-    if (r1 - r0 >= kParallelRecordsMin) HostPool::get().run(r1 - r0, fill);
-    else fill(0, r1 - r0);
+    c_.stats.sha_wait_ms += ms_since(tw);
+    tr_.mark("wait");
+    auto tf = Clock::now();
+    zc_record* const rb = c_.recs.data() + r0;
+    for (const uint64_t x : gq) memcpy(rb[x >> 32].sha1, gsha + 20 * (uint32_t)x, 16);
     for (size_t j = 0; j < idx.size(); ++j) memcpy(c_.recs[idx[j]].sha1, &sh[j * 20], 16);
-    // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_
-    fresh_sha_.resize(16 * fresh_.size());
-    {
-      size_t f = f0;
-      for (size_t i = r0; i < r1 && f < fresh_.size(); ++i) {
-        const zc_record& r = c_.recs[i];
-        if (r.kind == ZC_CHUNK_NEW && r.size == W_) memcpy(&fresh_sha_[16 * f++], r.sha1, 16);
-      }
+    tr_.mark("fill");
+    // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_: at
+    // the stream's end straight into the historic index (their entries
+    // hp.e0 + j), else kept with fresh_ until they join it
+    uint8_t* fs;
+    const bool in_place = stream_end && f0 == 0 && hp.k == frec.size();
+    if (in_place) {
+      c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
+      fs = c_.hsha.data() + 16 * (size_t)hp.e0;
+    } else {
+      fresh_sha_.resize(16 * fresh_.size());
+      fs = fresh_sha_.data() + 16 * f0;
     }
+    for (size_t j = 0; j < frec.size(); ++j) memcpy(fs + 16 * j, rb[frec[j]].sha1, 16);
     c_.nrec_done = r1;
-    if (stream_end) stream_end_index(&hp);
+    c_.stats.sha_fill_ms += ms_since(tf);
+    tr_.mark("fresh_sha");
+    th = Clock::now();
+    if (stream_end) stream_end_index(&hp, in_place);
+    c_.stats.hist_ms += ms_since(th);
+    tr_.mark("hist_sha");
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
@@ -2226,9 +2448,9 @@ class Resolver {
   // matches a committed one's index (chunk_index.cc:26-79).  Without it the
   // index is left as the stream found it (entries evicted from the window
   // during the stream are dropped again).
-  void stream_end_index(const HistPending* hp) {
+  void stream_end_index(const HistPending* hp, bool sha_in_place = false) {
     if (c_.flags & ZC_FLAG_SHA1) {
-      hist_add_sha(*hp, fresh_sha_.data());
+      hist_add_sha(*hp, sha_in_place ? nullptr : fresh_sha_.data());
     } else {
       index_truncate(c_, hist0_, statics0_);
     }
@@ -2431,7 +2653,11 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_sha, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_lead, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_list, hipEventDisableTiming));
     HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
+    HCK(hipStreamCreateWithFlags(&c->sha_stream2, hipStreamNonBlocking));
+    HCK(hipEventCreateWithFlags(&c->ev_sha2, hipEventDisableTiming));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
   if (rc != ZC_OK) {
@@ -2457,8 +2683,13 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->ev_sha) (void)hipEventDestroy(c->ev_sha);
+    if (c->ev_lead) (void)hipEventDestroy(c->ev_lead);
+    if (c->ev_list) (void)hipEventDestroy(c->ev_list);
     if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
+    if (c->sha_stream2) (void)hipStreamSynchronize(c->sha_stream2);
+    if (c->sha_stream2) (void)hipStreamDestroy(c->sha_stream2);
+    if (c->ev_sha2) (void)hipEventDestroy(c->ev_sha2);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     lzo_scratch_free(c->lzo);
