@@ -168,44 +168,16 @@ struct Cand {  // anchor-probe candidate: window ending at p may equal chunk ref
 // without an anchor; CNT_CLASS: refs that are not the leader of their class
 // CNT_PAIRS: equal-key pairs to byte-check; CNT_SPAIRS: pairs of grid chunks
 // whose SHA-1 the side stream computes (ZC_FLAG_SHA1), decided by SHA-1 prefix
-// CNT_SHAL: grid chunks listed for the SHA-1 by the class leads (EpochIndex::sha_list)
 enum { CNT_POOL = 0, CNT_OVERFLOW = 1, CNT_CAND = 2, CNT_RUNS = 3, CNT_FOVF = 4, CNT_ANCLESS = 5, CNT_CLASS = 6,
-       CNT_PAIRS = 7, CNT_SPAIRS = 8, CNT_SHAL = 9, CNT_LAST = 10 };
+       CNT_PAIRS = 7, CNT_SPAIRS = 8, CNT_LAST = 9 };
 
 // --- launchers (return hipError_t of the launch) ---------------------------
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s);
 // the same in pieces: full 2 MiB tiles [tile0, tile0 + ntiles), then the
 // partial last tile (if any); the pieces may run as the stream arrives
-// beside: the 128-VGPR variant, for a scan that shares the CUs with the grid
-// SHA-1 (ZC_FLAG_SHA1): two waves of each kernel fit on every SIMD whichever is
-// dispatched first (the 137-VGPR scan cannot find room once the SHA-1 waves hold
-// the CUs, and then waits for them: 5.9 instead of 1.6 ms per 8 GiB)
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
-                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s, bool beside);
-
-// ZC_FLAG_SHA1 with the whole stream in one scan launch: the scan's own lanes
-// also hash the stream's whole grid chunks [q W, (q + 1) W), q < nchunks, two
-// 64-byte SHA-1 blocks per scan round (zc_scan_sha_kernel), instead of a
-// separate SHA-1 kernel beside the scan
-struct ShaFuse {
-  uint8_t* out20;    // SHA-1 of chunk q at out20 + 20 q
-  uint64_t nchunks;  // whole grid chunks
-  uint32_t W;        // a multiple of 128
-};
-// lanes of a scan launch over ntiles tiles (one chunk or more each when fused)
-uint64_t scan_lanes(uint64_t ntiles);
-// fused when every lane has a chunk (the SHA-1 then spreads evenly over the
-// scan's rounds) and the chunks are whole 128-byte steps
-inline bool sha_fusable(uint64_t n, uint32_t W, uint64_t ntiles) {
-  return W >= 128 && W % 128 == 0 && ntiles && n / W >= scan_lanes(ntiles);
-}
-hipError_t launch_scan_sha(const uint8_t* data, uint64_t n, uint64_t ntiles, int32_t anchor_lo, uint64_t* blk,
-                           PoolOut po, unsigned long long* counters, const ShaFuse& sf, hipStream_t s);
-// SHA-1 of the single range [base, base + len) into out20 + 20 idx
-hipError_t launch_sha1_one(const uint8_t* data, uint64_t base, uint32_t len, uint32_t idx, uint8_t* out20,
-                           hipStream_t s);
-
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s);
 hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                             unsigned long long* counters, hipStream_t s);
 
@@ -253,26 +225,14 @@ struct EpochIndex {
   uint2* pairs;  // scratch: nref {ref, leader} pairs for the byte check
   const uint8_t* gsha;  // null: every pair by bytes
   uint64_t n_gsha;
-  // ZC_FLAG_SHA1, classes first: every ref that leads its key (no lower ref
-  // with an equal key) and is a whole grid chunk q < sha_nfull appends q here
-  // (counters[CNT_SHAL]); the grid SHA-1 then hashes those chunks only, and a
-  // chunk byte-equal to its leader takes the leader's digest (null: no list)
-  uint32_t* sha_list;
-  uint64_t sha_nfull;
 };
-// ev_lead (optional): recorded after the class leads, before the byte checks
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
-                              hipStream_t s, hipEvent_t ev_lead = nullptr);
-// SHA-1 (20 bytes at out20 + 20 q) of the grid chunks q = tail_q0 .. tail_q0 +
-// ntail - 1 (the last possibly partial, n bytes in all) and of the whole grid
-// chunks q = list[t], t0 <= t < min(*count, t1) (*count: a device counter)
-hipError_t launch_sha1_list(const uint8_t* data, uint64_t n, uint32_t W, const uint32_t* list,
-                            const unsigned long long* count, uint32_t t0, uint32_t t1, uint64_t tail_q0,
-                            uint32_t ntail, uint8_t* out20, hipStream_t s);
+                              hipStream_t s);
 // the SHA-1 pairs of the last launch_epoch_index (counters[CNT_SPAIRS]): key +
 // SHA-1-prefix equality (ChunkIndex::findChunk's test, chunk_index.cc:119-143)
-// decides the class; gsha must be complete (ordered after the SHA-1 kernel)
+// decides the class; gsha must be complete (ordered after the SHA-1 kernel),
+// or null: every such pair joins its class (a speculation checked later)
 hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, uint32_t W, const EpochIndex& ix,
                             uint32_t nref, hipStream_t s);
 uint32_t probe_filter_words();

@@ -37,6 +37,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <exception>
 #include <condition_variable>
@@ -64,6 +65,9 @@ struct ZcError {
   int code;
   std::string msg;
 };
+// a speculative SHA-1 class join proved wrong (Resolver::spec_): redo the
+// stream without speculation
+struct Respeculate {};
 
 #define HCK(x)                                                                         \
   do {                                                                                 \
@@ -267,29 +271,108 @@ class HostPool {
   bool stop_ = false;
 };
 
+// Three helper threads for a short job that follows a wait: arm() wakes them
+// before the wait (a sleeping thread's wake-up costs more than the job
+// itself: the records' SHA-1 fill took 0.4-1.0 ms on the host pool against
+// 0.2 ms on one thread), they spin until run() hands them their parts (or
+// until the deadline passes, then sleep again).
+class SpinTeam {
+ public:
+  static SpinTeam& get() {
+    static std::mutex mk;
+    static SpinTeam* team = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> lk(mk);
+    if (!team || owner != getpid()) {
+      team = new SpinTeam;
+      owner = getpid();
+    }
+    return *team;
+  }
+  // the helpers spin for at most `ms` from now
+  void arm(double ms = 8.0) {
+    deadline_.store(now_ns() + (int64_t)(ms * 1e6), std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      ++wake_;
+    }
+    cv_.notify_all();
+  }
+  // f(begin, end) over [0, n) in kParts parts; the helpers that are not
+  // spinning (not armed, or past the deadline) are not waited for: their
+  // parts run on this thread
+  void run(size_t n, const std::function<void(size_t, size_t)>& f) {
+    std::lock_guard<std::mutex> one(run_);
+    job_ = &f;
+    n_ = n;
+    for (auto& c : claim_) c.store(0, std::memory_order_release);  // (job_, n_ published with it)
+    done_.store(0, std::memory_order_relaxed);
+    seq_.fetch_add(1, std::memory_order_release);
+    int mine = 0;
+    for (int k = 0; k < kParts; ++k)  // claim every part nobody took yet, from the last
+      if (claim_[kParts - 1 - k].exchange(1, std::memory_order_acq_rel) == 0) {
+        part(kParts - 1 - k);
+        ++mine;
+      }
+    while (done_.load(std::memory_order_acquire) + mine < kParts) _mm_pause();
+    job_ = nullptr;
+  }
+
+ private:
+  static constexpr int kHelpers = 3, kParts = kHelpers + 1;
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  SpinTeam() {
+    for (int w = 0; w < kHelpers; ++w) th_.emplace_back([this, w] { loop(w); });
+    for (auto& t : th_) t.detach();  // process lifetime
+  }
+  void part(int k) {
+    const size_t a = n_ * k / kParts, b = n_ * (k + 1) / kParts;
+    if (b > a) (*job_)(a, b);
+  }
+  void loop(int w) {
+    uint64_t woken = 0, seen = seq_.load();
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return wake_ != woken; });
+        woken = wake_;
+      }
+      // spin until a job appears or the deadline passes
+      while (now_ns() < deadline_.load(std::memory_order_relaxed)) {
+        const uint64_t s = seq_.load(std::memory_order_acquire);
+        if (s != seen) {
+          seen = s;
+          if (claim_[w].exchange(1, std::memory_order_acq_rel) == 0) {
+            part(w);
+            done_.fetch_add(1, std::memory_order_release);
+          }
+          break;
+        }
+        _mm_pause();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex run_, m_;
+  std::condition_variable cv_;
+  uint64_t wake_ = 0;
+  std::atomic<int64_t> deadline_{0};
+  std::atomic<uint64_t> seq_{0};
+  std::atomic<int> claim_[kParts];
+  std::atomic<int> done_{0};
+  const std::function<void(size_t, size_t)>* job_ = nullptr;
+  size_t n_ = 0;
+};
+
 // records of grid chunks k0 .. k0 + n - 1 of an epoch at r0 (offset r0 + k W,
 // size W, one kind, rolling hash key[k] or 0), in parallel when many: two
 // 40-byte records are five 16-byte words, streamed past the caches (no
 // read-for-ownership of the lines they overwrite)
 constexpr uint64_t kParallelRecordsMin = 32768;
 
-// diagnostics (ZC_TRACE=1): host phase times of the stream end, to stderr
-struct Trace {
-  bool on = getenv("ZC_TRACE") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  std::string line;
-  void mark(const char* what) {
-    if (!on) return;
-    const auto n = std::chrono::steady_clock::now();
-    char b[64];
-    snprintf(b, sizeof b, " %s=%.3f", what, std::chrono::duration<double, std::milli>(n - t).count());
-    line += b;
-    t = n;
-  }
-  ~Trace() {
-    if (on && !line.empty()) fprintf(stderr, "zc_trace:%s\n", line.c_str());
-  }
-};
 void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uint32_t W, uint32_t kind,
                        const uint64_t* key) {
   auto fill = [&](size_t a, size_t b) {
@@ -332,12 +415,8 @@ struct zc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host -> HBM copies overlapped with the scan
   hipStream_t sha_stream = nullptr;   // SHA-1 of the grid chunks, beside the scan (ZC_FLAG_SHA1)
-  hipStream_t sha_stream2 = nullptr;  // the early part of a listed grid SHA-1
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   hipEvent_t ev_sha = nullptr;  // the grid chunks' SHA-1 (sha_stream) are complete
-  hipEvent_t ev_lead = nullptr;  // the first epoch's class leads (and SHA-1 list) are complete
-  hipEvent_t ev_list = nullptr;  // ... and the list is on the host
-  hipEvent_t ev_sha2 = nullptr;  // the early part of the listed SHA-1 is complete
   std::string err;
 
   // host feed
@@ -408,10 +487,8 @@ struct zc_ctx {
   DevBuf<uint32_t> otiles, obase;
   DevBuf<unsigned long long> counters;
   DevBuf<uint8_t> gsha;  // SHA-1 of the first epoch's grid chunks (ZC_FLAG_SHA1)
+  HostBuf<uint2> h_pairs;  // an epoch's pairs of grid chunks joined by speculation
   HostBuf<uint8_t> h_gsha;  // ... copied back on the SHA-1 stream right behind the kernel
-  DevBuf<uint32_t> sha_list;  // the grid chunks the class leads list for the SHA-1
-  DevBuf<unsigned long long> sha_cnt;  // their count, copied out of the counters (later epochs clear those)
-  HostBuf<uint32_t> h_shalist;
   HostBuf<uint64_t> h_hmkey;  // pinned staging of the keys and anchors of new historic entries
   HostBuf<uint32_t> h_hmanc;
   DevBuf<uint64_t> c_start, c_key, c_fp, c_vis;
@@ -585,7 +662,6 @@ class Resolver {
   }
   void drain() {
     (void)hipStreamSynchronize(c_.sha_stream);
-    (void)hipStreamSynchronize(c_.sha_stream2);
     (void)hipStreamSynchronize(c_.copy_stream);
     (void)hipStreamSynchronize(c_.stream);
   }
@@ -610,10 +686,6 @@ class Resolver {
     hist0_ = c_.nhist;
     statics0_ = c_.statics.size();
     r_ = s_ = x_resume_ = hspan_ = 0;
-    fused_sha_ = sha_deferred_ = false;
-    sha_classes_ = sha_listed_ = sha_counted_ = false;
-    shal_n_ = 0;
-    sha_src_.clear();
     scan_setup();
   }
   // bytes [0, n) of the stream are (being) copied to the device, in order on
@@ -630,20 +702,8 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
-      const bool sha = !windowed_ && (c_.flags & ZC_FLAG_SHA1) && indexable_ && sha_mode() == 1;
-      if (!windowed_ && (c_.flags & ZC_FLAG_SHA1) && indexable_ && sha_mode() == 0 && tiles_done_ == 0 && t1 == n_ / ZC_STILE && sha_fusable(n_, W_, t1)) {
-        // the whole stream in one launch: the scan's lanes hash the grid
-        // chunks too (pre_sha() adds a partial last chunk)
-        const uint64_t k = (n_ + W_ - 1) / W_;
-        c_.gsha.ensure(k * 20);
-        HCK(launch_scan_sha(d_, n_, t1, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
-                            ShaFuse{c_.gsha.p, n_ / W_, W_}, c_.stream));
-        fused_sha_ = true;
-      } else {
-        // with chunk ids of a whole-stream run the grid SHA-1 shares the CUs
-        HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(),
-                              c_.counters.p, c_.stream, sha));
-      }
+      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
+                            c_.stream));
       tiles_done_ = t1;
     }
   }
@@ -801,7 +861,6 @@ class Resolver {
       HCK(hipMemcpyAsync(c_.hfp.p + e0, c_.c_fp.p + r0, run * sizeof(uint64_t), hipMemcpyDeviceToDevice, c_.stream));
       memcpy(c_.hkey.data() + e0, c_.h_key.p + (r0 - dev_nconf_), run * sizeof(uint64_t));
     }
-    tr_.mark("hm_run");
     if (run < k) {
       const uint32_t kr = k - run;  // entries e0 + run + t, t < kr
       c_.hm_key.ensure(kr);
@@ -853,13 +912,11 @@ class Resolver {
       sync(c_);
       memcpy(c_.hkey.data() + eb, c_.h_hmkey.p, kr * sizeof(uint64_t));
     }
-    tr_.mark("hm_rest");
     // the entries' anchors, for hist_add_sha (it synchronises first)
     d2h(c_, c_.h_hmanc.p, c_.hanc.p + e0, k);
     hp.anc = c_.h_hmanc.p;
     c_.nhist = e0 + k;
     hist_table(c_, e0);
-    tr_.mark("hm_table");
     hp.e0 = e0;
     hp.k = k;
     return hp;
@@ -1181,19 +1238,12 @@ class Resolver {
         c_.ckeys.ensure(1u << tbits);
         c_.c_cls.ensure(nref_);
         c_.cpairs.ensure(nref_);
-        // classes first (sha_classes_): the stream's first epoch lists its
-        // leading grid chunks for the SHA-1, launched right behind the leads
-        const bool list_sha = sha_classes_ && !sha_listed_ && r_e_ == 0 && nconf_ == 0;
-        if (list_sha) c_.sha_list.ensure(std::max<uint32_t>(nsref, 1));
         ix = EpochIndex{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
                         c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
-                        pre_sha_n_ && !sha_classes_ && sha_mode() != 2 ? c_.gsha.p : nullptr, pre_sha_n_,
-                        list_sha ? c_.sha_list.p : nullptr, n_ / W_};
-        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream,
-                               list_sha ? c_.ev_lead : nullptr));
-        if (list_sha) sha_launch_listed(nsref);
+                        pre_sha_n_ ? c_.gsha.p : nullptr, pre_sha_n_};
+        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
         dev_nspec_ = nsref;
@@ -1210,7 +1260,7 @@ class Resolver {
         HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
                          c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
                          c_.stream));
-      sha_launch_deferred();
+      sha_launch();
       HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
       if (nsref)
         HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -1221,26 +1271,27 @@ class Resolver {
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       sync(c_);
       HCK(hipStreamSynchronize(c_.copy_stream));
-      if (sha_listed_ && !sha_counted_) {
-        shal_n_ = c_.h_cnt[CNT_SHAL];
-        sha_counted_ = true;
-      }
       if (scan_check()) {  // the pool changed under this epoch: queue it again
         c_.stats.epochs--;
-        // (the re-run rewrites the class arrays the listed SHA-1 may still read)
-        if (sha_listed_) {
-          HCK(hipStreamSynchronize(c_.sha_stream2));
-          HCK(hipStreamSynchronize(c_.sha_stream));
-        }
         return true;
       }
       if (nref_ && c_.h_cnt[CNT_SPAIRS]) {
         // ZC_FLAG_SHA1: equal-key grid chunks whose SHA-1 the side stream
         // computes are decided by key + SHA-1 prefix, as ChunkIndex::findChunk
-        // decides (chunk_index.cc:119-143) -- no byte comparison -- once the
-        // SHA-1 kernel is done; the probe then runs again on the final classes
-        HCK(hipStreamWaitEvent(c_.stream, c_.ev_sha, 0));
-        HCK(launch_class_sha(c_.gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
+        // decides (chunk_index.cc:119-143) -- no byte comparison; the probe
+        // then runs again on the final classes.  Speculatively (spec_): joined
+        // now, the walk runs while the SHA-1 does, and finalize_records checks
+        // every such pair's prefixes once they are in (a pair that differs --
+        // equal 64-bit keys of different bytes -- redoes the stream without
+        // speculation: Respeculate); else after the SHA-1 kernel
+        const uint64_t nsp = c_.h_cnt[CNT_SPAIRS];
+        if (spec_) {
+          c_.h_pairs.ensure(nsp);
+          d2h(c_, c_.h_pairs.p, c_.cpairs.p + (nref_ - nsp), nsp);
+        } else {
+          HCK(hipStreamWaitEvent(c_.stream, c_.ev_sha, 0));
+        }
+        HCK(launch_class_sha(spec_ ? nullptr : c_.gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
         if (anchors) {
           HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
           HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
@@ -1249,11 +1300,15 @@ class Resolver {
         }
         d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
         sync(c_);
+        if (spec_)  // the pairs to check, as grid chunk numbers
+          for (uint64_t t = 0; t < nsp; ++t) {
+            const uint2 pr = c_.h_pairs.p[t];
+            spec_pairs_.push_back({ref_start(pr.x) / W_, ref_start(pr.y) / W_});
+          }
       }
       ncand = anchors ? c_.h_cnt[CNT_CAND] : 0;
       nancless = nref_ ? c_.h_cnt[CNT_ANCLESS] : 0;
       if (nref_ && c_.h_cnt[CNT_CLASS]) load_classes();
-      if (sha_listed_ && sha_src_.empty()) sha_sources(nsref);
       if (ncand > c_.cand.cap) {  // rare: rerun the probe into a buffer that fits
         c_.cand.ensure(ncand + 1024);
         HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
@@ -2192,10 +2247,16 @@ class Resolver {
   // workgroups); finalize() takes every record that is one of them from there
   uint64_t pre_sha_n_ = 0;
   bool gsha_ready_ = false;
+  // speculative SHA-1 class joins (whole-stream runs): the pairs of grid
+  // chunks joined before their digests existed
+  std::vector<std::pair<uint64_t, uint64_t>> spec_pairs_;
+ public:
+  bool spec_ = false;
+ private:
   const uint8_t* grid_sha() {
     if (!gsha_ready_) {
-      sha_launch_deferred();
-      if (pre_sha_n_) HCK(hipStreamSynchronize(c_.sha_stream));  // (ordered after sha_stream2's part)  // the kernel and the copy behind it
+      sha_launch();  // (if no epoch batch queued it)
+      if (pre_sha_n_) HCK(hipStreamSynchronize(c_.sha_stream));  // the kernel and the copy behind it  // the kernel and the copy behind it
       gsha_ready_ = true;
     }
     return c_.h_gsha.p;
@@ -2205,129 +2266,39 @@ class Resolver {
     if (!pre_sha_n_ || ws % W_) return nullptr;
     const uint64_t q = ws / W_;
     if (q >= pre_sha_n_ || ws + W_ > n_) return nullptr;
-    const uint8_t* g = grid_sha();  // (classes first: the sources are known once the SHA-1 is queued)
-    const uint32_t src = sha_slot(q);
-    return src == kNone ? nullptr : g + 20ull * src;
+    return grid_sha() + 20 * q;
   }
-  bool fused_sha_ = false;  // the scan launch hashes the whole grid chunks (launch_scan_sha)
-  bool sha_deferred_ = false;
-  // Classes first: the grid SHA-1 hashes only the chunks that lead their key
-  // in the stream's first epoch (and the grid chunks that are no refs); a
-  // chunk whose bytes the epoch verified equal to its leader's takes the
-  // leader's digest (sha_src_), one whose check failed is hashed with the
-  // records that are no grid chunks.  Duplicated content is hashed once.
-  bool sha_classes_ = false, sha_listed_ = false, sha_counted_ = false;
-  uint64_t shal_n_ = 0;
-  uint32_t sha_nsref_ = 0;
-  std::vector<uint32_t> sha_src_;  // grid chunk -> the chunk whose digest is its own (kNone: hash it)
-  // The listed SHA-1 in two parts.  Early, right behind the class leads and
-  // beside the rest of the epoch's batch: the grid chunks after the refs and
-  // the first kEarlySha listed ones -- at most a few waves, too few to hold
-  // the SIMDs the batch's latency-bound kernels need (a full SHA-1 grid beside
-  // them stretched the probe from 0.07 to 3.9 ms), and what is left when
-  // duplicated content lists few chunks (all-zero data lists one, whose 64 KiB
-  // chain then hashes while the byte checks run).  Late, behind the batch
-  // (sha_launch_deferred): the rest of the list.
-  static constexpr uint32_t kEarlySha = 1024;
-  void sha_launch_listed(uint32_t nsref) {
-    sha_listed_ = true;
-    sha_nsref_ = nsref;
-    const uint64_t k = pre_sha_n_;
-    c_.h_shalist.ensure(std::max<uint32_t>(nsref, 1));
-    c_.sha_cnt.ensure(1);
-    HCK(hipStreamWaitEvent(c_.sha_stream2, c_.ev_lead, 0));
-    HCK(hipMemcpyAsync(c_.sha_cnt.p, c_.counters.p + CNT_SHAL, sizeof(unsigned long long), hipMemcpyDeviceToDevice,
-                       c_.sha_stream2));
-    if (nsref) {
-      HCK(hipMemcpyAsync(c_.h_shalist.p, c_.sha_list.p, nsref * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                         c_.sha_stream2));
-      HCK(hipEventRecord(c_.ev_list, c_.sha_stream2));
-    }
-    HCK(launch_sha1_list(d_, n_, W_, c_.sha_list.p, c_.sha_cnt.p, 0, std::min(nsref, kEarlySha), nsref,
-                         (uint32_t)(k - nsref), c_.gsha.p, c_.sha_stream2));
-    HCK(hipEventRecord(c_.ev_sha2, c_.sha_stream2));
-    sha_deferred_ = nsref > kEarlySha;  // the rest behind the batch
-    if (!sha_deferred_) {
-      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha2, 0));
-      HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
-      HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
-    }
-  }
-  // after the first epoch's classes are known (cls_, empty: no class has
-  // members): the digest source of every grid chunk
-  void sha_sources(uint32_t nsref) {
-    const uint64_t k = pre_sha_n_;
-    sha_src_.assign(k, kNone);
-    if (nsref) HCK(hipEventSynchronize(c_.ev_list));
-    for (uint64_t t = 0; t < shal_n_; ++t) sha_src_[c_.h_shalist.p[t]] = c_.h_shalist.p[t];
-    for (uint64_t q = nsref; q < k; ++q) sha_src_[q] = (uint32_t)q;
-    if (!cls_.empty())
-      for (uint32_t q = 0; q < nsref && q < cls_.size(); ++q)
-        if (sha_src_[q] == kNone && cls_[q] != q && sha_src_[cls_[q]] == cls_[q]) sha_src_[q] = cls_[q];
-  }
-  // the chunk whose digest slot holds grid chunk q's SHA-1, or kNone
-  uint32_t sha_slot(uint64_t q) const {
-    if (!sha_classes_) return (uint32_t)q;
-    return q < sha_src_.size() ? sha_src_[q] : kNone;
-  }
-  // experiment: ZC_SHA_MODE 0 fused (default), 1 a SHA-1 kernel beside the scan,
-  // 2 a SHA-1 kernel behind the first epoch's batch
-  int sha_mode() const {
-    const char* e = getenv("ZC_SHA_MODE");
-    return e ? atoi(e) : 0;
-  }
-  void sha_launch_deferred() {
-    if (!sha_deferred_) return;
-    sha_deferred_ = false;
-    const uint64_t k = pre_sha_n_;
-    HCK(hipEventRecord(c_.ev_sha, c_.stream));
-    HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
-    if (sha_listed_) {
-      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_list, 0));  // the count copied out (sha_stream2)
-      HCK(launch_sha1_list(d_, n_, W_, c_.sha_list.p, c_.sha_cnt.p, kEarlySha, sha_nsref_, 0, 0, c_.gsha.p,
-                           c_.sha_stream));
-      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha2, 0));
-    } else {
-      HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
-    }
-    HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
-    HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
-  }
+  // The grid SHA-1 is VALU work (~630 instructions per 64-byte block, 2.6 ms
+  // per 8 GiB alone) and runs on its own stream behind the first epoch's
+  // batch (sha_launch, queued right after the batch's last kernel): beside
+  // the scan it only got the cycles the older scan waves left (scan + SHA-1
+  // as concurrent kernels 4.1 ms, fused into the scan 4.3 ms, one after the
+  // other 4.2 ms), and the batch's latency-bound kernels beside it starved
+  // (chunk metadata 1.2 ms instead of 25 us, the probe 3.9 ms instead of
+  // 0.1).  After the batch the walk, the records and the index registration
+  // run on the host while the SHA-1 does.
+  bool sha_pending_ = false;
   void pre_sha() {
     pre_sha_n_ = 0;
     gsha_ready_ = false;
+    sha_pending_ = false;
     if (!(c_.flags & ZC_FLAG_SHA1) || !indexable_ || n_ < W_) return;
     const uint64_t k = (n_ + W_ - 1) / W_;
     if (k > 0xFFFFFFFFull) return;
     c_.gsha.ensure(k * 20);
     c_.h_gsha.ensure(k * 20);
-    if (fused_sha_) {
-      // done by the scan, on the context's stream; a partial last chunk here
-      if (n_ % W_) HCK(launch_sha1_one(d_, n_ / W_ * W_, (uint32_t)(n_ % W_), (uint32_t)(n_ / W_), c_.gsha.p,
-                                       c_.stream));
-      HCK(hipEventRecord(c_.ev_sha, c_.stream));
-      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
-    } else if (sha_mode() == 2) {
-      sha_deferred_ = true;  // launched behind the first epoch's batch (sha_launch_deferred)
-      pre_sha_n_ = k;
-      return;
-    } else if (sha_mode() == 5 && W_ % 16 == 0) {
-      sha_classes_ = true;  // launched behind the first epoch's class leads (sha_launch_listed)
-      pre_sha_n_ = k;
-      return;
-    } else if (sha_mode() == 1) {
-      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_in, 0));
-      HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
-      HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
-    } else {
-      // behind the scan (not beside it), ahead of the epoch's batch
-      HCK(hipEventRecord(c_.ev_sha, c_.stream));
-      HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
-      HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
-      HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
-    }
-    HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
     pre_sha_n_ = k;
+    sha_pending_ = true;
+  }
+  void sha_launch() {
+    if (!sha_pending_) return;
+    sha_pending_ = false;
+    const uint64_t k = pre_sha_n_;
+    HCK(hipEventRecord(c_.ev_sha, c_.stream));  // behind the batch (and the scan)
+    HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
+    HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+    HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
+    HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
   }
 
   // ---------------------------------------------------------------- finalize
@@ -2335,7 +2306,6 @@ class Resolver {
   // and (ZC_FLAG_SHA1) every chunk record its SHA-1 prefix.
   std::vector<uint64_t> fresh_;  // NEW W-byte chunks of the stream still resident: offset,
   std::vector<uint8_t> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
-  Trace tr_;
   // stream_end: the stream's end (run_final): with ZC_FLAG_SHA1 its new W-byte
   // chunks join the context's index here, their device metadata queued before
   // the wait for the grid SHA-1, so that wait ends the call with little after it
@@ -2346,7 +2316,6 @@ class Resolver {
       Clock::time_point t;
       ~Done() { st.finalize_ms += ms_since(t); }
     } done{c_.stats, t0};
-    if (stream_end) tr_.mark("to_finalize");
     std::vector<uint64_t> a, b;
     std::vector<size_t> rest;
     for (size_t i = 0; i < need_digest_.size(); ++i) {
@@ -2394,32 +2363,35 @@ class Resolver {
         frec.push_back((uint32_t)(i - r0));
       }
       const uint64_t q = grid_q(r);
-      const uint32_t src = q != kInf ? sha_slot(q) : kNone;
-      if (src != kNone) {
-        gq.push_back((uint64_t)(i - r0) << 32 | src);
+      if (q != kInf) {
+        gq.push_back((uint64_t)(i - r0) << 32 | q);
         continue;
       }
       sa.push_back(r.offset);
       sl.push_back(r.size);
       idx.push_back(i);
     }
-    tr_.mark("rec_loop");
     std::vector<uint8_t> sh = sha1s(sa, sl);
-    tr_.mark("sha1s");
     HistPending hp;
     auto th = Clock::now();
     if (stream_end) hp = hist_add_meta(fresh_);
-    tr_.mark("hist_meta");
     c_.stats.hist_ms += ms_since(th);
+    const bool team = gq.size() >= kParallelRecordsMin;
+    if (team) SpinTeam::get().arm();  // awake by the time the digests land
     auto tw = Clock::now();
     const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;  // waits for the side stream
     c_.stats.sha_wait_ms += ms_since(tw);
-    tr_.mark("wait");
+    for (const auto& pq : spec_pairs_)  // the speculated joins (epoch)
+      if (memcmp(gsha + 20 * pq.first, gsha + 20 * pq.second, 16) != 0) throw Respeculate{};
+    spec_pairs_.clear();
     auto tf = Clock::now();
     zc_record* const rb = c_.recs.data() + r0;
-    for (const uint64_t x : gq) memcpy(rb[x >> 32].sha1, gsha + 20 * (uint32_t)x, 16);
+    auto fill = [&](size_t a, size_t b) {
+      for (size_t j = a; j < b; ++j) memcpy(rb[gq[j] >> 32].sha1, gsha + 20 * (uint32_t)gq[j], 16);
+    };
+    if (team) SpinTeam::get().run(gq.size(), fill);
+    else fill(0, gq.size());
     for (size_t j = 0; j < idx.size(); ++j) memcpy(c_.recs[idx[j]].sha1, &sh[j * 20], 16);
-    tr_.mark("fill");
     // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_: at
     // the stream's end straight into the historic index (their entries
     // hp.e0 + j), else kept with fresh_ until they join it
@@ -2432,14 +2404,16 @@ class Resolver {
       fresh_sha_.resize(16 * fresh_.size());
       fs = fresh_sha_.data() + 16 * f0;
     }
-    for (size_t j = 0; j < frec.size(); ++j) memcpy(fs + 16 * j, rb[frec[j]].sha1, 16);
+    auto fcopy = [&](size_t a, size_t b) {
+      for (size_t j = a; j < b; ++j) memcpy(fs + 16 * j, rb[frec[j]].sha1, 16);
+    };
+    if (team && frec.size() >= kParallelRecordsMin) SpinTeam::get().run(frec.size(), fcopy);
+    else fcopy(0, frec.size());
     c_.nrec_done = r1;
     c_.stats.sha_fill_ms += ms_since(tf);
-    tr_.mark("fresh_sha");
     th = Clock::now();
     if (stream_end) stream_end_index(&hp, in_place);
     c_.stats.hist_ms += ms_since(th);
-    tr_.mark("hist_sha");
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
@@ -2653,11 +2627,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_sha, hipEventDisableTiming));
-    HCK(hipEventCreateWithFlags(&c->ev_lead, hipEventDisableTiming));
-    HCK(hipEventCreateWithFlags(&c->ev_list, hipEventDisableTiming));
     HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
-    HCK(hipStreamCreateWithFlags(&c->sha_stream2, hipStreamNonBlocking));
-    HCK(hipEventCreateWithFlags(&c->ev_sha2, hipEventDisableTiming));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
   if (rc != ZC_OK) {
@@ -2683,13 +2653,8 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->ev_sha) (void)hipEventDestroy(c->ev_sha);
-    if (c->ev_lead) (void)hipEventDestroy(c->ev_lead);
-    if (c->ev_list) (void)hipEventDestroy(c->ev_list);
     if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
-    if (c->sha_stream2) (void)hipStreamSynchronize(c->sha_stream2);
-    if (c->sha_stream2) (void)hipStreamDestroy(c->sha_stream2);
-    if (c->ev_sha2) (void)hipEventDestroy(c->ev_sha2);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     lzo_scratch_free(c->lzo);
@@ -2834,8 +2799,24 @@ int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
     HCK(hipEventRecord(c->ev_in, nullptr));
     HCK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
     c->windowed_last = false;
-    Resolver res(*c, (const uint8_t*)d_data, n, false);
-    res.run();
+    const uint32_t nh = c->nhist;
+    const size_t ns = c->statics.size();
+    bool redo = false;
+    {
+      Resolver res(*c, (const uint8_t*)d_data, n, false);
+      res.spec_ = (c->flags & ZC_FLAG_SHA1) != 0;
+      try {
+        res.run();
+      } catch (const Respeculate&) {
+        res.drain();
+        redo = true;
+      }
+    }
+    if (redo) {  // (equal 64-bit keys of different grid chunks: practically only by construction)
+      index_truncate(*c, nh, ns, true);
+      Resolver res(*c, (const uint8_t*)d_data, n, false);
+      res.run();
+    }
     c->d_last = (const uint8_t*)d_data;
     c->n_last = n;
     c->finished = true;

@@ -207,7 +207,7 @@ enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, 
        ABL_DMA_NT = 512, ABL_DMA_SC1 = 1024, ABL_STAGGER_HALF = 2048, ABL_STAGGER_QUARTER = 4096,
        ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768,
        ABL_TE_DIGEST_NT = 65536, ABL_TE_DIGEST_SAME = 131072, ABL_PRIO = 262144,
-       ABL_DWORD_SAMPLED = 524288 /* timing only: anchors tested at dword ends only */ };
+       ABL_DWORD_SAMPLED = 524288 /* timing only: anchors tested at dword ends only (experiment 16) */ };
 // the product's scan: the staging DMA is non-temporal (the stream is read
 // once; tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB)
 constexpr int kScanProduct = ABL_DMA_NT;
@@ -237,7 +237,7 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 // (ABL_DWORD_SAMPLED, timing only: the gear tested at dword ends alone -- a
 // quarter of the positions -- saves 6 % of the kernel, but windows at other
 // alignments then need every chunk's anchors in four residues, whose search
-// costs more than that: DESIGN 4.1.)
+// costs more than that: DESIGN 4.1, experiment 16.)
 template <int ABL>
 __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr, ScanLane& s, WaveList& wl,
                                            uint32_t& last) {
@@ -690,87 +690,10 @@ struct ScanLds {
   uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
   uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 3];
 };
-
-// The fused SHA-1 of the grid chunks (zc_scan_sha_kernel, ZC_FLAG_SHA1).  The
-// grid SHA-1 is VALU work (~610 instructions per 64-byte block) and the scan
-// leaves ~30 % of the VALU idle waiting for its DMA rounds; as a second kernel
-// beside the scan the SHA-1 waves only got the cycles the older scan waves
-// left and the resolver's kernels behind the scan starved in turn (chunk
-// metadata 1.15 ms instead of 25 us, profiles/r04_c2sha_kernel_trace.csv).
-// Fused, every scan lane owns grid chunks g, g + L, g + 2L, ... (L = lanes of
-// the launch, nchunks >= L) and hashes two blocks (128 bytes, one cache line)
-// of the current one per scan round: the loads are issued after the round's
-// wait and consumed at the round's end, so they ride in the same in-order
-// vmcnt as the DMA (only round R + 2's DMA is issued after them).  The block
-// counter is wave-uniform: every lane is at the same offset of its chunk.
-__device__ __forceinline__ void sha1_block(uint32_t* st, const uint32_t* wbe);
-__device__ __forceinline__ v4u32 global_read16_nt(const uint8_t* p) {
-  v4u32 v;
-  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-struct ShaLane {
-  uint32_t st[5];
-  uint64_t chunk;      // the lane's current chunk (>= nchunks: hashed, not stored)
-  const uint8_t* cur;  // its first byte (the last chunk's when past the end)
-  uint32_t bi;         // wave-uniform: next block of the chunk
-  uint32_t b, nb;      // wave-uniform: blocks done, blocks of the wave's first lane
-};
-__device__ __forceinline__ void sha1_reset(uint32_t (&st)[5]) {
-  st[0] = 0x67452301u;
-  st[1] = 0xEFCDAB89u;
-  st[2] = 0x98BADCFEu;
-  st[3] = 0x10325476u;
-  st[4] = 0xC3D2E1F0u;
-}
-__device__ __forceinline__ void sha_lane_at(ShaLane& sl, const uint8_t* __restrict__ data, const ShaFuse& sf) {
-  sl.cur = data + (sl.chunk < sf.nchunks ? sl.chunk : sf.nchunks - 1) * (uint64_t)sf.W;
-}
-template <int SHA>
-__device__ __forceinline__ void sha_issue(const ShaLane& sl, v4u32 (&sd)[8]) {
-  const uint8_t* p = sl.cur + (uint64_t)sl.bi * 64;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) sd[j] = SHA == 2 ? global_read16_nt(p + 16 * j) : global_read16(p + 16 * j);
-}
-// two blocks of landed bytes; at the chunk's end its padding block and the
-// 20-byte digest (big-endian words, as SHA1() writes it)
-__device__ __forceinline__ void sha_step(ShaLane& sl, const v4u32 (&sd)[8], const uint8_t* __restrict__ data,
-                                         uint64_t lanes, const ShaFuse& sf) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) w[4 * k + q] = __builtin_bswap32(sd[4 * h + k][q]);
-    sha1_block(sl.st, w);
-  }
-  sl.bi += 2;
-  sl.b += 2;
-  if (sl.bi == sf.W / 64) {
-    uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = 0;
-    w[0] = 0x80000000u;
-    w[15] = sf.W * 8u;  // W < 2^29
-    sha1_block(sl.st, w);
-    if (sl.chunk < sf.nchunks) {
-      uint32_t* o = (uint32_t*)(sf.out20 + sl.chunk * 20);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) o[k] = __builtin_bswap32(sl.st[k]);
-    }
-    sha1_reset(sl.st);
-    sl.chunk += lanes;
-    sl.bi = 0;
-    sha_lane_at(sl, data, sf);
-  }
-}
-
-template <int ABL, int SHA = 0>  // SHA: 0 none, 1 fused SHA-1 (temporal loads), 2 (non-temporal loads)
+template <int ABL>
 __device__ __forceinline__ void scan_body(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
-    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L,
-    const ShaFuse& sf = ShaFuse{nullptr, 0, 0}) {
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L) {
   auto& ring = L.ring;
   auto& wlist = L.wlist;
   auto& wdata = L.wdata;
@@ -822,17 +745,6 @@ __device__ __forceinline__ void scan_body(
   uint32_t tail_stores = 0;  // global stores the last tile end left in flight
   uint32_t last = kNoEntry;  // this lane's newest entry in the wave's list
   uint32_t acc_pool = 0, acc_over = 0;  // wave-uniform: anchors stored, wave-tiles overflowed
-  ShaLane sl{};
-  v4u32 sd[8];
-  const uint64_t lanes = (uint64_t)grid * ZC_SCAN_TPB;
-  if (SHA) {
-    const uint64_t g0 = (uint64_t)blockIdx.x * ZC_SCAN_TPB + wave * 64;  // the wave's first lane
-    const uint64_t m0 = sf.nchunks > g0 ? (sf.nchunks - g0 + lanes - 1) / lanes : 0;
-    sl.nb = __builtin_amdgcn_readfirstlane((uint32_t)(m0 * (sf.W / 64)));
-    sl.chunk = g0 + lane;
-    sha_lane_at(sl, data, sf);
-    sha1_reset(sl.st);
-  }
 
 #pragma unroll 1
   for (uint32_t R = 0; R < nR; ++R) {
@@ -869,8 +781,6 @@ __device__ __forceinline__ void scan_body(
           for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
     }
-    const bool sha_round = SHA && sl.b < sl.nb;  // wave-uniform
-    if (sha_round) sha_issue<SHA>(sl, sd);
     static_assert(kPieces == 8, "the round is read in two halves of four pieces");
     v4u32 va[4], vb[4];
 #pragma unroll
@@ -896,29 +806,7 @@ __device__ __forceinline__ void scan_body(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (sha_round) {
-      // this round's SHA-1 loads have landed once only what was issued after
-      // them is outstanding: round R + 2's DMA and, before a half's first
-      // round, its warm-up loads
-      if (R + 2 >= nR) wait_vmcnt<0>();
-      else if ((R + 2) % kHalfRounds == 0 && !(ABL & ABL_NO_WARM)) wait_vmcnt<kDmaRound + 2>();
-      else wait_vmcnt<kDmaRound>();
-      ties(sd);
-      sha_step(sl, sd, data, lanes, sf);
-    }
     if (tile_end) tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
-  }
-  if (SHA) {
-    // blocks the rounds did not cover (a workgroup with fewer tiles, or more
-    // than two blocks per round of chunk): plain loads
-    wait_vmcnt<0>();
-#pragma unroll 1
-    while (sl.b < sl.nb) {
-      sha_issue<SHA>(sl, sd);
-      wait_vmcnt<0>();
-      ties(sd);
-      sha_step(sl, sd, data, lanes, sf);
-    }
   }
   if (!(ABL & ABL_NO_ATOMIC) && lane == 0) {
     if (acc_pool) atomicAdd(&counters[CNT_POOL], (unsigned long long)acc_pool);
@@ -933,26 +821,6 @@ __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
   __shared__ ScanLds lds;
   scan_body<ABL>(data, n, tile0, ntiles, lo_thr, blk, po, counters, lds);
 }
-// The scan with the grid chunks' SHA-1 fused in (ShaFuse, zc_device.h)
-template <int ABL, int SHA = 1>
-__global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_sha_kernel(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
-    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ShaFuse sf) {
-  __shared__ ScanLds lds;
-  scan_body<ABL, SHA>(data, n, tile0, ntiles, lo_thr, blk, po, counters, lds, sf);
-}
-// The same with at most 128 VGPRs, so two waves of another kernel (the grid
-// SHA-1 beside the scan) fit on each SIMD next to the scan's two.  The LDS is
-// dynamic (sizeof(ScanLds) at launch): with a static 160 KiB the compiler
-// derives two waves per SIMD from it and ignores the register bound.
-template <int ABL>
-__global__ void __launch_bounds__(ZC_SCAN_TPB, 2) zc_scan_kernel_v128(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
-    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t zc_dyn_lds[];
-  scan_body<ABL>(data, n, tile0, ntiles, lo_thr, blk, po, counters, *(ScanLds*)zc_dyn_lds);
-}
-
 // the stream's last, partial tile: one 256-thread block per wave-tile, a
 // 1 KiB sub-span per thread (block digests and anchors)
 __global__ void __launch_bounds__(ZC_WT_BLOCK) zc_scan_tail_kernel(const uint8_t* __restrict__ data, uint64_t n,
@@ -1534,36 +1402,17 @@ __global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint
 __global__ void __launch_bounds__(256) zc_class_lead_kernel(
     const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off, uint32_t nref,
     const uint64_t* __restrict__ ckeys, uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
-    uint2* __restrict__ pairs, unsigned long long* __restrict__ counters, ShaGrid sg, const uint64_t* __restrict__ start,
-    uint32_t* __restrict__ sha_list, uint64_t sha_nfull, uint32_t W) {
+    uint2* __restrict__ pairs, unsigned long long* __restrict__ counters, ShaGrid sg, const uint64_t* __restrict__ start) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t lead = 0;
-  if (i < nref) {
-    const uint64_t k = key[i];
-    const uint32_t mask = (1u << cbits) - 1;
-    uint64_t w;
-    for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {  // the key's slot: equal high word and an
-      w = ckeys[h];                                                 // equal key at its ref
-      if ((w >> 32) == (k >> 32) && key[(uint32_t)w] == k) break;
-    }
-    lead = (uint32_t)w;
-  }
-  if (sha_list) {
-    // a leading whole grid chunk is listed for the SHA-1 (one counter
-    // atomic per wave; the list's order does not matter)
-    const uint64_t c = i < nref ? start[i] : 0, q = c / W;
-    const bool lists = i < nref && lead == i && q * W == c && q < sha_nfull;
-    const uint64_t bal = __ballot(lists);
-    if (bal) {
-      const int first = __builtin_ctzll(bal);
-      uint32_t base = 0;
-      if ((threadIdx.x & 63) == (uint32_t)first)
-        base = (uint32_t)atomicAdd(&counters[CNT_SHAL], (unsigned long long)__popcll(bal));
-      base = __shfl(base, first, 64);
-      if (lists) sha_list[base + lane_prefix(bal)] = (uint32_t)q;
-    }
-  }
   if (i >= nref) return;
+  const uint64_t k = key[i];
+  const uint32_t mask = (1u << cbits) - 1;
+  uint64_t w;
+  for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {  // the key's slot: equal high word and an
+    w = ckeys[h];                                                 // equal key at its ref
+    if ((w >> 32) == (k >> 32) && key[(uint32_t)w] == k) break;
+  }
+  const uint32_t lead = (uint32_t)w;
   cls[i] = i;
   if (lead == i) {
     if (anc_missing(anc_off, i)) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = i;
@@ -1580,6 +1429,9 @@ __global__ void __launch_bounds__(256) zc_class_lead_kernel(
 // SHA-1 prefix (their 64-bit keys are equal already): key + prefix equality is
 // ChunkIndex::findChunk's own test (chunk_index.cc:119-143), so no bytes are
 // read.  Equal -> cls = leader; else a ref without an anchor goes to the screen.
+// sg.sha null: every pair joined before the SHA-1 exists (the resolver's
+// speculation; it checks the prefixes once they are in and redoes the stream
+// if one differs)
 __global__ void __launch_bounds__(256) zc_class_sha_kernel(ShaGrid sg, const uint64_t* __restrict__ start,
                                                            const uint32_t* __restrict__ anc_off, uint32_t nref,
                                                            uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
@@ -1591,8 +1443,12 @@ __global__ void __launch_bounds__(256) zc_class_sha_kernel(ShaGrid sg, const uin
   uint2 pr = make_uint2(0, 0);
   if (live) {
     pr = pairs[nref - 1 - t];
-    const uint4 a = sg.prefix(start[pr.x]), b = sg.prefix(start[pr.y]);
-    same = a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+    if (sg.sha) {
+      const uint4 a = sg.prefix(start[pr.x]), b = sg.prefix(start[pr.y]);
+      same = a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+    } else {
+      same = true;
+    }
     if (same) cls[pr.x] = pr.y;
     else if (anc_missing(anc_off, pr.x)) ancless[atomicAdd(&counters[CNT_ANCLESS], 1ull)] = pr.x;
   }
@@ -2616,26 +2472,6 @@ __global__ __launch_bounds__(64) void zc_sha1_grid16_kernel(const uint8_t* __res
   if (i < nr) sha1_range16(data, (uint64_t)i * W, W, i, out);
 }
 
-// Lane u < ntail: grid chunk tail_q0 + u (the chunks after the refs, a last
-// one possibly partial); lane u >= ntail: the listed whole chunk list[t],
-// t = t0 + u - ntail, t < min(*count, t1)
-__global__ __launch_bounds__(64) void zc_sha1_list_kernel(const uint8_t* __restrict__ data, uint64_t n, uint32_t W,
-                                                          const uint32_t* __restrict__ list,
-                                                          const unsigned long long* __restrict__ count, uint32_t t0,
-                                                          uint32_t t1, uint64_t tail_q0, uint32_t ntail,
-                                                          uint8_t* __restrict__ out) {
-  const uint32_t u = blockIdx.x * 64 + threadIdx.x;
-  if (u < ntail) {
-    const uint64_t q = tail_q0 + u, c = q * W;
-    sha1_range(data, c, (uint32_t)(n - c < W ? n - c : W), (uint32_t)q, out);
-    return;
-  }
-  const uint64_t t = (uint64_t)t0 + (u - ntail), cnt = *count;
-  if (t >= cnt || t >= t1) return;
-  const uint32_t q = list[t];
-  sha1_range16(data, (uint64_t)q * W, W, q, out);
-}
-
 // one range by value (the stream's last, partial grid chunk)
 __global__ __launch_bounds__(64) void zc_sha1_one_kernel(const uint8_t* __restrict__ data, uint64_t base, uint32_t L,
                                                          uint32_t i, uint8_t* __restrict__ out) {
@@ -2680,33 +2516,11 @@ static int cu_count() {
 }
 
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
-                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s, bool beside) {
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
   if (!ntiles) return hipSuccess;
   const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
-  if (beside)
-    hipLaunchKernelGGL(zc_scan_kernel_v128<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), sizeof(ScanLds), s, data, n,
-                       tile0, ntiles, anchor_lo, blk, po, counters);
-  else
-    hipLaunchKernelGGL(zc_scan_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles,
-                       anchor_lo, blk, po, counters);
-  return hipGetLastError();
-}
-
-uint64_t scan_lanes(uint64_t ntiles) { return std::min<uint64_t>(ntiles, (uint64_t)cu_count()) * ZC_SCAN_TPB; }
-
-hipError_t launch_scan_sha(const uint8_t* data, uint64_t n, uint64_t ntiles, int32_t anchor_lo, uint64_t* blk,
-                           PoolOut po, unsigned long long* counters, const ShaFuse& sf, hipStream_t s) {
-  if (!ntiles || !sha_fusable(n, sf.W, ntiles) || sf.nchunks > n / sf.W || !sf.out20 || ((uintptr_t)data & 15))
-    return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
-  hipLaunchKernelGGL(zc_scan_sha_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, (uint64_t)0,
-                     ntiles, anchor_lo, blk, po, counters, sf);
-  return hipGetLastError();
-}
-
-hipError_t launch_sha1_one(const uint8_t* data, uint64_t base, uint32_t len, uint32_t idx, uint8_t* out20,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(zc_sha1_one_kernel, dim3(1), dim3(64), 0, s, data, base, len, idx, out20);
+  hipLaunchKernelGGL(zc_scan_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles,
+                     anchor_lo, blk, po, counters);
   return hipGetLastError();
 }
 
@@ -2720,7 +2534,7 @@ hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, 
 
 hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                        unsigned long long* counters, hipStream_t s) {
-  hipError_t e = launch_scan_tiles(data, n, 0, n / ZC_STILE, anchor_lo, blk, po, counters, s, false);
+  hipError_t e = launch_scan_tiles(data, n, 0, n / ZC_STILE, anchor_lo, blk, po, counters, s);
   if (e != hipSuccess) return e;
   return launch_scan_tail(data, n, anchor_lo, blk, po, counters, s);
 }
@@ -2740,7 +2554,7 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
 
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
-                              hipStream_t s, hipEvent_t ev_lead) {
+                              hipStream_t s) {
   const uint32_t nref = nconf + nsref;
   const EpochClear ec{ix.ckeys, nref ? 1u << ix.cbits : 0u, ix.tab,
                       ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters};
@@ -2755,11 +2569,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                      ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
   hipLaunchKernelGGL(zc_class_lead_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, nref,
                      ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.pairs, ix.counters,
-                     ShaGrid{ix.gsha, ix.gsha ? ix.n_gsha : 0, n, W}, ix.start, ix.sha_list, ix.sha_nfull, W);
-  if (ev_lead) {
-    const hipError_t e = hipEventRecord(ev_lead, s);
-    if (e != hipSuccess) return e;
-  }
+                     ShaGrid{ix.gsha, ix.gsha ? ix.n_gsha : 0, n, W}, ix.start);
   // persistent: up to 16 waves per CU (the pair count is on the device)
   const unsigned vblocks = (unsigned)std::min<uint64_t>(blocks_for(nref, 4), (uint64_t)cu_count() * 4);
   hipLaunchKernelGGL(zc_class_verify_kernel, dim3(vblocks), dim3(256), 0, s, data, ix.start, ix.anc, W, ix.cls,
@@ -2769,7 +2579,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
 
 hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, uint32_t W, const EpochIndex& ix,
                             uint32_t nref, hipStream_t s) {
-  if (!nref || !gsha) return hipSuccess;
+  if (!nref) return hipSuccess;
   hipLaunchKernelGGL(zc_class_sha_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ShaGrid{gsha, n_gsha, n, W},
                      ix.start, ix.anc, nref, ix.cls, ix.ancless, ix.pairs, ix.counters);
   return hipGetLastError();
@@ -2974,17 +2784,6 @@ hipError_t launch_sha1_grid(const uint8_t* data, uint64_t n, uint32_t W, uint32_
   if (whole < nr)
     hipLaunchKernelGGL(zc_sha1_one_kernel, dim3(1), dim3(64), 0, s, data, (uint64_t)whole * W,
                        (uint32_t)(n - (uint64_t)whole * W), whole, out20);
-  return hipGetLastError();
-}
-
-hipError_t launch_sha1_list(const uint8_t* data, uint64_t n, uint32_t W, const uint32_t* list,
-                            const unsigned long long* count, uint32_t t0, uint32_t t1, uint64_t tail_q0,
-                            uint32_t ntail, uint8_t* out20, hipStream_t s) {
-  const uint64_t lanes = (uint64_t)ntail + (t1 > t0 ? t1 - t0 : 0);
-  if (!lanes) return hipSuccess;
-  if (W % 16 || ((uintptr_t)data & 15)) return hipErrorInvalidValue;  // the aligned whole-chunk path
-  hipLaunchKernelGGL(zc_sha1_list_kernel, dim3(blocks_for(lanes, 64)), dim3(64), 0, s, data, n, W, list, count, t0,
-                     t1, tail_q0, ntail, out20);
   return hipGetLastError();
 }
 
