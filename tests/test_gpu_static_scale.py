@@ -3,7 +3,7 @@ registers every chunk of every index file (chunk_index.cc:26-79) and findChunk
 probes all of them at every byte (chunk_index.cc:119-143).  Ids known only by
 value (no bytes, no anchors) go through the exact screen; past 2048 keys it
 tests a Bloom filter at every position and trims its runs on the device to
-exact 64-bit key hits.  Seeded with 3,000 / 300,000 random ids plus the real
+exact 64-bit key hits.  Seeded with 3,000 / 300,000 / 1 M / 2 M random ids plus the real
 ids of a block and of the all-zero chunk that the stream contains: records
 bit-exact vs the oracle (device-resident and through the feed window)."""
 import numpy as np
@@ -50,7 +50,7 @@ def _seeds(nrand):
 SPEC = "R5:30000000,R9:8000000,Z:1000000,R6:20000000,C40000000:3000000,R9:3000000"
 
 
-@pytest.mark.parametrize("nrand", [3000, 300000])
+@pytest.mark.parametrize("nrand", [3000, 300000, 1000000, 2000000])
 def test_large_static_index_device_vs_oracle(torch_cuda, nrand):
     from zbackup_amd import BackupCreator
     seeds, nreal = _seeds(nrand)

@@ -2,7 +2,7 @@
 (an index loaded from earlier backups, no content): how the exact screen's
 key map behaves as K grows.  Tooling only.
 
-  python tools/debug/static_scale.py [GiB] K1 K2 ...
+  python tools/static_scale.py [GiB] K1 K2 ...
 """
 import os
 import sys
@@ -11,7 +11,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from zbackup_amd import BackupCreator, fill_splitmix64  # noqa: E402
 
 

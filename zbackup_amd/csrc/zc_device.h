@@ -114,19 +114,25 @@ struct PoolOut {
 inline uint32_t bloom_bits_for(size_t keys) {
   // a block per two keys up to 512 K keys (300 K keys -> 2 MiB, half an XCD's
   // L2: ~8e-5 false hits per position, screened out on the device by the
-  // 64-bit run filter), a block per key beyond (1 M keys -> 8 MiB: ~5e-5)
+  // 64-bit run filter), a block per key beyond (1 M keys -> 8 MiB: ~5e-5).
+  // (Two keys per block past 512 K -- 1 M keys in 4 MiB -- let 15x the false
+  // hits through, 6e-4 per position: the runs they open cost more than the
+  // L2 misses of the larger filter, 22 vs 107 GiB/s)
   uint32_t b = 17;
   while (b < 24 && ((size_t)(keys > (512u << 10) ? 1 : 2) << b) < keys) ++b;
   return b;
 }
 // The Bloom buffer: 2^bits blocks of two words, then a 2^19-bit first level
-// (one bit per key, from the high word of key * golden) that the staged
+// (one bit per key, from the low word of key * golden) that the staged
 // screen holds in LDS: positions whose bit is clear skip the block gather
 constexpr uint32_t kBloomPfBits = 19;
 constexpr uint32_t kBloomPfWords = 1u << (kBloomPfBits - 5);
 inline size_t bloom_words(uint32_t bits) { return ((size_t)2 << bits) + kBloomPfWords; }
+// (from the LOW word of key * golden, the block from its high word: a first
+// level on the block index's own bits let through positions whose block
+// then shared bits with a key's -- 15x the false hits at 1 M keys)
 __host__ __device__ inline uint32_t bloom_pf(uint64_t key) {
-  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & ((1u << kBloomPfBits) - 1u);
+  return (uint32_t)(key * 0x9E3779B97F4A7C15ull) >> (32 - kBloomPfBits);
 }
 __host__ __device__ inline uint32_t bloom_block(uint64_t key, uint32_t bits) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));

@@ -2005,9 +2005,10 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
             for (int q = 0; q < 4; ++q) {
               V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xo[p][d] >> (8 * q)) & 0xFFu) * K.pw64;
               const uint64_t key = V64 + K.pw64;
-              // bloom_block and bloom_pf: the high word of key * golden
-              const uint32_t hi = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32);
-              const uint32_t f = hi & ((1u << kBloomPfBits) - 1u);
+              // bloom_block: the high word of key * golden; bloom_pf: the low word's top bits
+              const uint64_t kg = key * 0x9E3779B97F4A7C15ull;
+              const uint32_t hi = (uint32_t)(kg >> 32);
+              const uint32_t f = (uint32_t)kg >> (32 - kBloomPfBits);
               bi[4 * d + q] = hi >> bsh;
               pw[4 * d + q] = s_pf[f >> 5] >> (f & 31u);
               gs[pi][4 * d + q] = bloom_seed(key);
