@@ -106,8 +106,8 @@ typedef struct {
   uint64_t hist_entries; /* historic index entries (chunks whose bytes have left HBM) */
   /* parts of finalize_ms (ZC_FLAG_SHA1): */
   double sha_wait_ms;    /* blocked on the grid chunks' SHA-1 and its copy to the host */
-  double sha_fill_ms;    /* SHA-1 prefixes into the records (and the new chunks' list) */
-  double hist_ms;        /* the stream's new chunks joining the context's index */
+  double sha_fill_ms;    /* after it: SHA-1 prefixes into the records, the new chunks' index entries completed */
+  double hist_ms;        /* before it: the stream's new chunks joining the context's index (keys, anchors) */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;

@@ -2410,10 +2410,8 @@ class Resolver {
     if (team && frec.size() >= kParallelRecordsMin) SpinTeam::get().run(frec.size(), fcopy);
     else fcopy(0, frec.size());
     c_.nrec_done = r1;
-    c_.stats.sha_fill_ms += ms_since(tf);
-    th = Clock::now();
     if (stream_end) stream_end_index(&hp, in_place);
-    c_.stats.hist_ms += ms_since(th);
+    c_.stats.sha_fill_ms += ms_since(tf);
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
