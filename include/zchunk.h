@@ -108,6 +108,7 @@ typedef struct {
   double sha_wait_ms;    /* blocked on the grid chunks' SHA-1 and its copy to the host */
   double sha_fill_ms;    /* after it: SHA-1 prefixes into the records, the new chunks' index entries completed */
   double hist_ms;        /* before it: the stream's new chunks joining the context's index (keys, anchors) */
+  uint64_t respeculations; /* streams redone because a speculative key + SHA-1 class join proved wrong */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;

@@ -2814,6 +2814,7 @@ int zc_chunk_device(zc_ctx* c, const void* d_data, uint64_t n) {
       index_truncate(*c, nh, ns, true);
       Resolver res(*c, (const uint8_t*)d_data, n, false);
       res.run();
+      c->stats.respeculations = 1;
     }
     c->d_last = (const uint8_t*)d_data;
     c->n_last = n;
