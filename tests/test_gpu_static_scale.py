@@ -2,8 +2,10 @@
 registers every chunk of every index file (chunk_index.cc:26-79) and findChunk
 probes all of them at every byte (chunk_index.cc:119-143).  Ids known only by
 value (no bytes, no anchors) go through the exact screen; past 2048 keys it
-tests a Bloom filter at every position and trims its runs on the device to
-exact 64-bit key hits.  Seeded with 3,000 / 300,000 / 1 M / 2 M random ids plus the real
+tests a Bloom filter at every position: up to 640 K keys two levels (LDS, then
+L2) whose runs are trimmed on the device to exact 64-bit key hits, beyond that
+one level whose hits are checked in the kernel against a table of 16-bit check
+words.  Seeded with 3,000 / 300,000 / 1 M / 2 M random ids plus the real
 ids of a block and of the all-zero chunk that the stream contains: records
 bit-exact vs the oracle (device-resident and through the feed window)."""
 import numpy as np
@@ -63,9 +65,10 @@ def test_large_static_index_device_vs_oracle(torch_cuda, nrand):
         _same(bc.records(), want)
 
 
-def test_large_static_index_window_vs_oracle(torch_cuda):
+@pytest.mark.parametrize("nrand", [300000, 1000000])
+def test_large_static_index_window_vs_oracle(torch_cuda, nrand):
     from zbackup_amd import BackupCreator
-    seeds, _ = _seeds(300000)
+    seeds, _ = _seeds(nrand)
     data = oracle.gen(SPEC)
     want = oracle.chunk_array(data, W64, seeds=seeds)
     with BackupCreator(W64, seeds=seeds, sha1=True, window=1) as bc:
@@ -74,19 +77,20 @@ def test_large_static_index_window_vs_oracle(torch_cuda):
         _same(bc.records(), want)
 
 
-@pytest.mark.parametrize("W", [1000, 4099, 300007])
-def test_bloom_screen_odd_w_vs_oracle(torch_cuda, W):
-    """The Bloom mode of the staged screen (over 2048 by-value keys) at chunk
-    sizes whose out-byte funnel shifts differ (-W mod 16 = 8, 13, 9), on a
-    stream long enough (> 64 MiB) for the staged kernel to run."""
+@pytest.mark.parametrize("W,nrand", [(1000, 3000), (4099, 3000), (300007, 3000), (1000, 700000), (4099, 700000)])
+def test_bloom_screen_odd_w_vs_oracle(torch_cuda, W, nrand):
+    """The Bloom mode of the staged screen (over 2048 by-value keys; two
+    levels, and one level past 640 K) at chunk sizes whose out-byte funnel
+    shifts differ (-W mod 16 = 8, 13, 9), on a stream long enough (> 64 MiB)
+    for the staged kernel to run."""
     from zbackup_amd import BackupCreator
     old = oracle.gen("R9:8000000")
     real = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(old, W) if k == "N" and s == W][:400]
     zero = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(oracle.gen(f"Z:{W}"), W)]
     rng = np.random.default_rng(W)
-    keys = rng.integers(1, 2**63, 3000, dtype=np.int64)
-    shas = rng.integers(0, 256, (3000, 16), dtype=np.uint8)
-    seeds = real + zero + [(shas[i].tobytes(), int(keys[i]), W) for i in range(3000)]
+    keys = rng.integers(1, 2**63, nrand, dtype=np.int64)
+    shas = rng.integers(0, 256, (nrand, 16), dtype=np.uint8)
+    seeds = real + zero + [(shas[i].tobytes(), int(keys[i]), W) for i in range(nrand)]
     data = oracle.gen("R5:40000000,R9:8000000,Z:1000000,R6:30000000,C41000000:3000000")
     want = oracle.chunk_array(data, W, seeds=seeds)
     assert (want["kind"] == 1).sum() >= len(real)

@@ -111,7 +111,17 @@ struct PoolOut {
 // Blocked Bloom filter of the exact screen's large key sets (more than the
 // LDS holds), over the full 64-bit window keys: 2^bits blocks of two 32-bit
 // words (8 bytes, one gather), a key sets three bits in each word
+// Past kBloomOneLevelMin keys the LDS first level below passes most positions
+// (85 % at 1 M keys): the screen then gathers every position's block from a
+// filter sized for an XCD's L2 (~8 keys per block, 2 MiB at 2 M keys) and
+// checks the filter's hits in the check table (chk_* below)
+constexpr size_t kBloomOneLevelMin = 640u << 10;
 inline uint32_t bloom_bits_for(size_t keys) {
+  if (keys >= kBloomOneLevelMin) {
+    uint32_t b = 18;
+    while (b < 24 && ((size_t)8 << b) < keys) ++b;
+    return b;
+  }
   // a block per two keys up to 512 K keys (300 K keys -> 2 MiB, half an XCD's
   // L2: ~8e-5 false hits per position, screened out on the device by the
   // 64-bit run filter), a block per key beyond (1 M keys -> 8 MiB: ~5e-5).
@@ -150,6 +160,33 @@ __host__ __device__ inline uint32_t bloom_test(uint32_t x, uint32_t y, uint32_t 
   const uint32_t tx = (x >> (g & 31u)) & (x >> ((g >> 5) & 31u)) & (x >> ((g >> 10) & 31u));
   const uint32_t ty = (y >> ((g >> 15) & 31u)) & (y >> ((g >> 20) & 31u)) & (y >> ((g >> 25) & 31u));
   return tx & ty & 1u;
+}
+// The one-level screen's check table: 2^bits buckets of four 16-bit check
+// words (8 bytes, one read), then kChkPad buckets.  A key's bucket is the
+// high bits of key * golden (its Bloom block's bits, and more); its check
+// word the top half of bloom_seed (0 -> 1: 0 marks an empty slot).  A full
+// bucket overflows into the next; the pad buckets end every chain (the last
+// stays empty).  >= 16 slots per key: a bucket is full ~1e-4 of the time.
+constexpr uint32_t kChkPad = 64;
+__host__ __device__ inline uint32_t chk_word_of_seed(uint32_t g) {
+  const uint32_t c = g >> 16;
+  return c ? c : 1u;
+}
+__host__ __device__ inline uint32_t chk_word(uint64_t key) { return chk_word_of_seed(bloom_seed(key)); }
+__host__ __device__ inline uint32_t chk_bucket(uint64_t key, uint32_t bits) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+// 1: c is in bucket v; 0: it is not and the bucket has an empty slot (so c
+// is not in the table); 2: the bucket is full without c (look on)
+__host__ __device__ inline uint32_t chk_match(uint2 v, uint32_t c) {
+  const uint32_t s0 = v.x & 0xFFFFu, s1 = v.x >> 16, s2 = v.y & 0xFFFFu, s3 = v.y >> 16;
+  if (s0 == c || s1 == c || s2 == c || s3 == c) return 1;
+  return (s0 == 0 || s1 == 0 || s2 == 0 || s3 == 0) ? 0 : 2;
+}
+inline uint32_t chk_bits_for(size_t keys) {
+  uint32_t b = 10;
+  while (((size_t)4 << b) < 16 * keys) ++b;
+  return b;
 }
 __host__ __device__ inline uint32_t bloom_lo(uint32_t g) {
   return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u)) | (1u << ((g >> 10) & 31u));
@@ -318,11 +355,19 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
 
 // the large-key-set screen: nf > 2048 keys go through the Bloom filter
 // `bloom` (2^bloom_bits uint2 blocks) of the 64-bit window key, rolled at
-// every position (the staged kernel's runs are then trimmed by key64_filter)
+// every position.  Two levels (chk null: the LDS first level, then the
+// block), its runs then trimmed by key64_filter; or one level: every position
+// gathers its block and the filter's hits are checked in the check table
+// `chk` (2^chk_bits + kChkPad buckets)
 hipError_t launch_fscan_staged_bloom(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                                      uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt,
-                                     const uint32_t* bloom, uint32_t bloom_bits, Run* runs, uint64_t runs_cap, uint64_t* wt_off,
+                                     const uint32_t* bloom, uint32_t bloom_bits, const uint16_t* chk,
+                                     uint32_t chk_bits, Run* runs, uint64_t runs_cap, uint64_t* wt_off,
                                      uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s);
+// add the 64-bit keys[0, n) to a check table (2^bits + kChkPad buckets); a
+// key that found no slot before the table's end sets *ovf
+hipError_t launch_chk_add(uint16_t* chk, uint32_t bits, const uint64_t* keys, uint32_t n, unsigned int* ovf,
+                          hipStream_t s);
 // set the bits of the 64-bit keys[0, n) in a Bloom filter
 hipError_t launch_bloom_add(uint32_t* bloom, uint32_t bits, const uint64_t* keys, uint32_t n, hipStream_t s);
 // Short screen runs (<= 64 positions) are trimmed to the positions whose

@@ -448,6 +448,12 @@ struct zc_ctx {
   std::vector<uint32_t> sc_fbits;  // zc_fscan's 2^19-bit map
   DevBuf<uint32_t> bloom_s, bloom_w;  // Bloom filter of the set (and per epoch with the epoch's keys)
   uint32_t bloom_bits = 0;
+  // the one-level screen (kBloomOneLevelMin keys and more): its check table
+  // (and per epoch with the epoch's keys), or none (the two-level screen)
+  DevBuf<uint16_t> chk_s, chk_w;
+  DevBuf<unsigned int> chk_ovf;
+  uint32_t chk_bits = 0;
+  bool bloom_one = false;
   DevBuf<uint64_t> kset;              // 64-bit keys, open addressing (empty = 0)
   uint32_t kset_bits = 0;
   int kset_zero = 0;
@@ -585,6 +591,31 @@ void statics_screen(zc_ctx& c) {
       }
   }
   c.bloom_s.ensure(bloom.size());
+  c.bloom_one = keys.size() + 64 >= kBloomOneLevelMin;
+  if (c.bloom_one) {
+    // room for the epochs' own keys too (launch_chk_add); a chain that would
+    // reach the last bucket makes the table twice as large
+    for (c.chk_bits = chk_bits_for(keys.size() + 65536);; ++c.chk_bits) {
+      const uint64_t nb = (1ull << c.chk_bits) + kChkPad;
+      std::vector<uint16_t> chk(nb * 4, 0);
+      bool fits = true;
+      for (uint64_t k : keys) {
+        const uint16_t cw = (uint16_t)chk_word(k);
+        uint64_t sl = (uint64_t)chk_bucket(k, c.chk_bits) * 4;
+        while (sl < (nb - 1) * 4 && chk[sl] != 0 && chk[sl] != cw) ++sl;
+        if (sl == (nb - 1) * 4) {
+          fits = false;
+          break;
+        }
+        chk[sl] = cw;
+      }
+      if (!fits) continue;
+      c.chk_s.ensure(chk.size());
+      h2d(c, c.chk_s.p, chk.data(), chk.size());
+      c.chk_ovf.ensure(1);
+      break;
+    }
+  }
   c.kset.ensure(set.size());
   c.kset_bits = bits;
   h2d(c, c.bloom_s.p, bloom.data(), bloom.size());
@@ -1571,12 +1602,14 @@ class Resolver {
     h2d(c_, c_.f32.p, keys32.data(), keys32.size());
     c_.fbits.ensure(1u << 14);
     bloom_p_ = nullptr;
+    chk_p_ = nullptr;
     if (bloom) {
       statics_screen(c_);
       std::vector<uint32_t> bits = c_.sc_fbits;
       for (uint32_t h : keys32) bits[h >> 18] |= 1u << ((h >> 13) & 31);
       h2d(c_, c_.fbits.p, bits.data(), bits.size());
       bloom_p_ = c_.bloom_s.p;
+      chk_p_ = c_.bloom_one ? c_.chk_s.p : nullptr;
       std::vector<uint64_t> fk;
       for (auto& kv : fmap_) fk.push_back(kv.first);
       std::sort(fk.begin(), fk.end());
@@ -1589,6 +1622,17 @@ class Resolver {
                            hipMemcpyDeviceToDevice, c_.stream));
         HCK(launch_bloom_add(c_.bloom_w.p, c_.bloom_bits, c_.flist.p, (uint32_t)fk.size(), c_.stream));
         bloom_p_ = c_.bloom_w.p;
+        if (c_.bloom_one) {  // and a copy of the check table
+          const size_t nw = ((1ull << c_.chk_bits) + kChkPad) * 4;
+          c_.chk_w.ensure(nw);
+          HCK(hipMemcpyAsync(c_.chk_w.p, c_.chk_s.p, sizeof(uint16_t) * nw, hipMemcpyDeviceToDevice, c_.stream));
+          HCK(hipMemsetAsync(c_.chk_ovf.p, 0, sizeof(unsigned int), c_.stream));
+          HCK(launch_chk_add(c_.chk_w.p, c_.chk_bits, c_.flist.p, (uint32_t)fk.size(), c_.chk_ovf.p, c_.stream));
+          unsigned int ovf = 0;
+          d2h(c_, &ovf, c_.chk_ovf.p, 1);
+          sync(c_);
+          chk_p_ = ovf ? nullptr : c_.chk_w.p;  // full: the two-level screen
+        }
       }
     } else if (nf > 16) {
       std::vector<uint32_t> bits(1u << 14, 0);
@@ -1648,7 +1692,8 @@ class Resolver {
       HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
       if (staged && bloom) {
         HCK(launch_fscan_staged_bloom(d_, n_, blk_v(), W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, bloom_p,
-                                      c_.bloom_bits, c_.runs.p, c_.runs.cap, fwt_off_v, fwt_cnt_v, c_.counters.p, c_.stream));
+                                      c_.bloom_bits, chk_p_, c_.chk_bits, c_.runs.p, c_.runs.cap, fwt_off_v,
+                                      fwt_cnt_v, c_.counters.p, c_.stream));
       } else if (staged) {
         HCK(launch_fscan_staged(d_, n_, blk_v(), W_, pw32, p_start, p_end, wt_lo, wt_hi - wt_lo, keys32.data(),
                                 c_.f32.p, nf, c_.fbits17.p, c_.runs.p, c_.runs.cap, fwt_off_v, fwt_cnt_v,
@@ -1730,6 +1775,7 @@ class Resolver {
   bool bloom_ = false;
   uint32_t nf_ = 0;
   const uint32_t* bloom_p_ = nullptr;
+  const uint16_t* chk_p_ = nullptr;  // the one-level screen's check table, or none
   // the screen runs lazily: positions [x0, fs_hi_) are screened so far, in
   // blocks of fs_len_ bytes (doubling) as the walk needs them
   bool fs_ready_ = false;

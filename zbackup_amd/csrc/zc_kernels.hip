@@ -1736,14 +1736,17 @@ __host__ __device__ constexpr uint32_t frow_swizzle(uint32_t row) { return (row 
 struct FKeys {
   uint32_t k[16];         // keys - 257^W (compared with V); unused slots repeat k[0]
   const uint32_t* dkeys;  // NF = 32: the nk keys, sorted (copied to LDS)
-  uint32_t nk;            // NF = 64: the Bloom filter's size, log2 blocks
-  const uint32_t* bloom;  // NF = 64: the Bloom filter (global memory, L2 resident)
-  uint64_t pw64;          // NF = 64: 257^W mod 2^64
+  uint32_t nk;            // NF >= 64: the Bloom filter's size, log2 blocks
+  const uint32_t* bloom;  // NF >= 64: the Bloom filter (global memory, L2 resident)
+  uint64_t pw64;          // NF >= 64: 257^W mod 2^64
+  const uint2* chk;       // NF = 65: the check table (buckets of four 16-bit check words)
+  uint32_t cbits;         // NF = 65: its size, log2 buckets (plus kChkPad)
 };
-// run slots per lane per wave-tile: the Bloom mode's false hits (~K / 6e9
-// per position) need more than the exact modes' two
+// run slots per lane per wave-tile: the two-level Bloom mode's false hits
+// (~K / 6e9 per position) need more than the exact modes' two; the one-level
+// mode's filter hits are checked in the kernel (~1e-5 of them left)
 template <int NF>
-constexpr int kFRS = NF == 64 ? 7 : kFRunSlots;
+constexpr int kFRS = NF == 64 ? 7 : NF == 65 ? 4 : kFRunSlots;
 // threads per workgroup: the Bloom mode runs 4 waves (one per SIMD; the
 // filter gathers, not latency, bound it) so the LDS holds its first level
 template <int NF>
@@ -1891,7 +1894,7 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
     // the out-bytes are the in-bytes another lane read a moment ago (W
     // earlier); their last use: in the Bloom mode marked non-temporal (nt),
     // so the streamed lines leave L2 to the filter
-    constexpr int kOutAux = NF == 64 ? 2 : 0;
+    constexpr int kOutAux = NF >= 64 ? 2 : 0;
 #pragma unroll
     for (int j = 0; j < kFDmaHalf; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rout, (lds_void_t*)(dst + kSlot + j * 1024), 16,
@@ -1939,7 +1942,7 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
           carry = make_uint4(w[0], w[1], w[2], w[3]);
         }
       }
-      if constexpr (NF == 64) V64 = ps < n ? rk_acc(data, blk, ps >= W ? ps - W : 0, ps) : 0;
+      if constexpr (NF >= 64) V64 = ps < n ? rk_acc(data, blk, ps >= W ? ps - W : 0, ps) : 0;
       head = wtbase < (uint64_t)W + 16;
       need_valid = wtbase < p_start || wtbase + ZC_FWT > p_end;
       open = false;
@@ -1959,7 +1962,7 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
       vst[p] = *(const uint4*)(slot + kSlot + lane * ZC_FROUND + ((p ^ sw) << 4));
     }
     wait_lgkmcnt<0>();  // the slot is free
-    if constexpr (NF == 64) {
+    if constexpr (NF >= 64) {
       // Bloom mode: the window values of the whole round first, then one
       // gather of a filter word per position, all in flight together and
       // issued before the next round's DMA (a later load could not be waited
@@ -1983,50 +1986,106 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
           }
         }
       }
-      // two halves of two pieces: 32 gathers in flight per lane each.  A
-      // position first tests the filter's first level in LDS; one whose bit
-      // is clear gathers block 0 instead of its own (all such lanes of the
-      // wave share one line), so the L2 gathers scale with the first level's
-      // fill, not with the positions
-      const uint2* const bl = (const uint2*)K.bloom;
-      const uint32_t bsh = 32u - K.nk;
+      if constexpr (NF == 64) {
+        // two halves of two pieces: 32 gathers in flight per lane each.  A
+        // position first tests the filter's first level in LDS; one whose bit
+        // is clear gathers block 0 instead of its own (all such lanes of the
+        // wave share one line), so the L2 gathers scale with the first level's
+        // fill, not with the positions
+        const uint2* const bl = (const uint2*)K.bloom;
+        const uint32_t bsh = 32u - K.nk;
+  #pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          uint2 bw[2][16];
+          uint32_t gs[2][16], pre[2];
+  #pragma unroll
+          for (int pi = 0; pi < 2; ++pi) {
+            const int p = 2 * hf + pi;
+            const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
+            uint32_t bi[16], pw[16];
+  #pragma unroll
+            for (int d = 0; d < 4; ++d)
+  #pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xo[p][d] >> (8 * q)) & 0xFFu) * K.pw64;
+                const uint64_t key = V64 + K.pw64;
+                // bloom_block: the high word of key * golden; bloom_pf: the low word's top bits
+                const uint64_t kg = key * 0x9E3779B97F4A7C15ull;
+                const uint32_t hi = (uint32_t)(kg >> 32);
+                const uint32_t f = (uint32_t)kg >> (32 - kBloomPfBits);
+                bi[4 * d + q] = hi >> bsh;
+                pw[4 * d + q] = s_pf[f >> 5] >> (f & 31u);
+                gs[pi][4 * d + q] = bloom_seed(key);
+              }
+            uint32_t pm = 0;
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              pm |= (pw[i] & 1u) << i;
+              bw[pi][i] = bl[(pw[i] & 1u) ? bi[i] : 0u];
+            }
+            pre[pi] = pm;
+          }
+  #pragma unroll
+          for (int pi = 0; pi < 2; ++pi) {
+            uint32_t m16 = 0;
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) m16 |= bloom_test(bw[pi][i].x, bw[pi][i].y, gs[pi][i]) << i;
+            hm[2 * hf + pi] = m16 & pre[pi];
+          }
+        }
+      } else {
+        // one level (large key sets, where an LDS first level passes nearly
+        // every position): every position gathers its block of an L2-sized
+        // filter (~8 keys per block: ~2 % false hits), and each filter hit
+        // reads the key's bucket of the check table (8 bytes): its check word
+        // there -- a hit; an empty slot -- a miss; a full bucket -- the next
+        // bucket.  A hit the check lets through falsely (~1e-5 of the filter's
+        // false hits) is a run the walk's exact key test drops.
+        const uint2* const bl = (const uint2*)K.bloom;
+        const uint32_t bsh = 32u - K.nk, csh = 32u - K.cbits;
+        // piece by piece (16 gathers in flight per lane, two waves per SIMD)
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        uint2 bw[2][16];
-        uint32_t gs[2][16], pre[2];
-#pragma unroll
-        for (int pi = 0; pi < 2; ++pi) {
-          const int p = 2 * hf + pi;
+        for (int p = 0; p < kFPieces; ++p) {
+          uint2 bw[16];
+          uint32_t gs[16], cb[16];
           const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
-          uint32_t bi[16], pw[16];
 #pragma unroll
           for (int d = 0; d < 4; ++d)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xo[p][d] >> (8 * q)) & 0xFFu) * K.pw64;
               const uint64_t key = V64 + K.pw64;
-              // bloom_block: the high word of key * golden; bloom_pf: the low word's top bits
-              const uint64_t kg = key * 0x9E3779B97F4A7C15ull;
-              const uint32_t hi = (uint32_t)(kg >> 32);
-              const uint32_t f = (uint32_t)kg >> (32 - kBloomPfBits);
-              bi[4 * d + q] = hi >> bsh;
-              pw[4 * d + q] = s_pf[f >> 5] >> (f & 31u);
-              gs[pi][4 * d + q] = bloom_seed(key);
+              const uint32_t hi = (uint32_t)((key * kGolden) >> 32);  // bloom_block, chk_bucket
+              gs[4 * d + q] = bloom_seed(key);
+              cb[4 * d + q] = hi >> csh;
+              bw[4 * d + q] = bl[hi >> bsh];
             }
-          uint32_t pm = 0;
+          uint32_t hx = 0;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            pm |= (pw[i] & 1u) << i;
-            bw[pi][i] = bl[(pw[i] & 1u) ? bi[i] : 0u];
+          for (int i = 0; i < 16; ++i) hx |= bloom_test(bw[i].x, bw[i].y, gs[i]) << i;
+          uint2 ev[16];
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((hx >> i) & 1u) ev[i] = K.chk[cb[i]];
+          uint32_t slow = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((hx >> i) & 1u) {
+              const uint32_t v = chk_match(ev[i], chk_word_of_seed(gs[i]));
+              if (v == 0) hx &= ~(1u << i);  // an empty slot: not in the set
+              else if (v == 2) slow |= 1u << i;  // a full bucket without it
+            }
+          if (__builtin_expect(__ballot(slow != 0) != 0, 0)) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if ((slow >> i) & 1u) {
+                const uint32_t c = chk_word_of_seed(gs[i]);
+                uint32_t b = cb[i] + 1, v;
+                while ((v = chk_match(K.chk[b], c)) == 2) ++b;  // the last pad bucket ends every chain
+                if (v == 0) hx &= ~(1u << i);
+              }
           }
-          pre[pi] = pm;
-        }
-#pragma unroll
-        for (int pi = 0; pi < 2; ++pi) {
-          uint32_t m16 = 0;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) m16 |= bloom_test(bw[pi][i].x, bw[pi][i].y, gs[pi][i]) << i;
-          hm[2 * hf + pi] = m16 & pre[pi];
+          hm[p] = hx;
         }
       }
       if (R + 2 < nR) issue(R + 2);
@@ -2695,6 +2754,7 @@ static hipError_t launch_fscan_staged_q(int nfk, unsigned grid, hipStream_t s, c
                      sbyte, p_start, p_end, wt0, nwt, K, fmap, runs, runs_cap, wt_off, wt_cnt, counters)
   if (nfk == 1) ZC_FS(1);
   else if (nfk == 64) ZC_FS(64);
+  else if (nfk == 65) ZC_FS(65);
   else if (nfk == 4) ZC_FS(4);
   else if (nfk == 16) ZC_FS(16);
   else if (nfk == 32) ZC_FS(32);
@@ -2732,26 +2792,31 @@ hipError_t launch_fscan_staged(const uint8_t* data, uint64_t n, const uint64_t* 
 
 hipError_t launch_fscan_staged_bloom(const uint8_t* data, uint64_t n, const uint64_t* blk, uint32_t W, uint32_t pw32,
                                      uint64_t p_start, uint64_t p_end, uint64_t wt0, uint64_t nwt,
-                                     const uint32_t* bloom, uint32_t bloom_bits, Run* runs, uint64_t runs_cap,
-                                     uint64_t* wt_off, uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
+                                     const uint32_t* bloom, uint32_t bloom_bits, const uint16_t* chk,
+                                     uint32_t chk_bits, Run* runs, uint64_t runs_cap, uint64_t* wt_off,
+                                     uint32_t* wt_cnt, unsigned long long* counters, hipStream_t s) {
   if (!nwt) return hipSuccess;
   if (W < 32 || n < 64 || p_end > n || (wt0 + nwt - 1) * ZC_FWT >= p_end || !bloom) return hipErrorInvalidValue;
+  if (bloom_bits < 1 || bloom_bits > 31 || (chk && (chk_bits < 1 || chk_bits > 31))) return hipErrorInvalidValue;
   FKeys K{};
   K.bloom = bloom;
   K.nk = bloom_bits;
   K.pw64 = pow257_dev(W);
+  K.chk = (const uint2*)chk;
+  K.cbits = chk_bits;
+  const int nfk = chk ? 65 : 64;
   const uint32_t m = (16u - W % 16u) % 16u;
-  constexpr unsigned kW64 = kFTPBn<64> / 64;
+  const unsigned kW64 = (chk ? kFTPBn<65> : kFTPBn<64>) / 64;
   const unsigned waves = (unsigned)std::min<uint64_t>(nwt, (uint64_t)cu_count() * kW64);
   const unsigned grid = (waves + kW64 - 1) / kW64;
   switch (m >> 2) {
-    case 0: return launch_fscan_staged_q<0>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+    case 0: return launch_fscan_staged_q<0>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                             nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
-    case 1: return launch_fscan_staged_q<1>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+    case 1: return launch_fscan_staged_q<1>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                             nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
-    case 2: return launch_fscan_staged_q<2>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+    case 2: return launch_fscan_staged_q<2>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                             nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
-    default: return launch_fscan_staged_q<3>(64, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
+    default: return launch_fscan_staged_q<3>(nfk, grid, s, data, n, blk, W, pw32, m & 3, p_start, p_end, wt0, nwt, K,
                                              nullptr, runs, runs_cap, wt_off, wt_cnt, counters);
   }
 }
@@ -2759,6 +2824,39 @@ hipError_t launch_fscan_staged_bloom(const uint8_t* data, uint64_t n, const uint
 hipError_t launch_bloom_add(uint32_t* bloom, uint32_t bits, const uint64_t* keys, uint32_t n, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(zc_bloom_add_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, bloom, bits, keys, n);
+  return hipGetLastError();
+}
+
+// the check table of a key set (thread per key): the key's check word into
+// the first empty slot from its bucket on (CAS on the slot's 32-bit word);
+// present already, or the table's end reached: done (the latter flagged)
+__global__ void zc_chk_add_kernel(uint16_t* __restrict__ chk, uint32_t bits, const uint64_t* __restrict__ keys,
+                                  uint32_t n, unsigned int* __restrict__ ovf) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = chk_word(keys[i]);
+  const uint64_t nslots = ((1ull << bits) + kChkPad - 1) * 4;  // the last bucket stays empty
+  for (uint64_t sl = (uint64_t)chk_bucket(keys[i], bits) * 4; sl < nslots; ++sl) {
+    unsigned int* w = (unsigned int*)(chk + (sl & ~1ull));
+    const uint32_t sh = (uint32_t)(sl & 1) * 16;
+    unsigned int old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const uint32_t cur = (old >> sh) & 0xFFFFu;
+      if (cur == c) return;
+      if (cur != 0) break;
+      const unsigned int want = old | (c << sh);
+      if (__hip_atomic_compare_exchange_strong(w, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        return;
+    }
+  }
+  atomicOr(ovf, 1u);
+}
+
+hipError_t launch_chk_add(uint16_t* chk, uint32_t bits, const uint64_t* keys, uint32_t n, unsigned int* ovf,
+                          hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(zc_chk_add_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, chk, bits, keys, n, ovf);
   return hipGetLastError();
 }
 
