@@ -2,7 +2,7 @@
 registers every chunk of every index file (chunk_index.cc:26-79) and findChunk
 probes all of them at every byte (chunk_index.cc:119-143).  Ids known only by
 value (no bytes, no anchors) go through the exact screen; past 2048 keys it
-tests a Bloom filter at every position: up to 640 K keys two levels (LDS, then
+tests a Bloom filter at every position: up to 384 K keys two levels (LDS, then
 L2) whose runs are trimmed on the device to exact 64-bit key hits, beyond that
 one level whose hits are checked in the kernel against a table of 16-bit check
 words.  Seeded with 3,000 / 300,000 / 1 M / 2 M random ids plus the real
@@ -80,7 +80,7 @@ def test_large_static_index_window_vs_oracle(torch_cuda, nrand):
 @pytest.mark.parametrize("W,nrand", [(1000, 3000), (4099, 3000), (300007, 3000), (1000, 700000), (4099, 700000)])
 def test_bloom_screen_odd_w_vs_oracle(torch_cuda, W, nrand):
     """The Bloom mode of the staged screen (over 2048 by-value keys; two
-    levels, and one level past 640 K) at chunk sizes whose out-byte funnel
+    levels, and one level past 384 K) at chunk sizes whose out-byte funnel
     shifts differ (-W mod 16 = 8, 13, 9), on a stream long enough (> 64 MiB)
     for the staged kernel to run."""
     from zbackup_amd import BackupCreator

@@ -112,10 +112,13 @@ struct PoolOut {
 // LDS holds), over the full 64-bit window keys: 2^bits blocks of two 32-bit
 // words (8 bytes, one gather), a key sets three bits in each word
 // Past kBloomOneLevelMin keys the LDS first level below passes most positions
-// (85 % at 1 M keys): the screen then gathers every position's block from a
-// filter sized for an XCD's L2 (~8 keys per block, 2 MiB at 2 M keys) and
-// checks the filter's hits in the check table (chk_* below)
-constexpr size_t kBloomOneLevelMin = 640u << 10;
+// (61 % at 500 K keys, 85 % at 1 M): the screen then gathers every position's
+// block from a filter sized for an XCD's L2 (~8 keys per block, 2 MiB at 2 M
+// keys) and checks the filter's hits in the check table (chk_* below).
+// Measured (1 GiB random, GiB/s, two levels / one level): 300 K 287 / 197,
+// 400 K 234 / 194, 500 K 26 / 191 (the two-level false hits overflow the run
+// slots), 800 K 117 / 190
+constexpr size_t kBloomOneLevelMin = 384u << 10;
 inline uint32_t bloom_bits_for(size_t keys) {
   if (keys >= kBloomOneLevelMin) {
     uint32_t b = 18;
