@@ -25,6 +25,8 @@ names), the same line carries, driver-observed:
   bundle_lzo   the bundle writer offload: saved chunks bundled (Writer::add),
                gathered and lzo1x_1-compressed on the GPU (bundle.cc:30-36,
                96-155), with liblzo2 on one core beside it
+  static_index the first GiB against 300 K and 2 M ids known by value only
+               (an index loaded from earlier backups, chunk_index.cc:26-79)
 """
 import argparse
 import json
@@ -249,6 +251,35 @@ def timed_steps(torch, world, step, warmup, steps):
     scan = [step() for _ in range(steps)]
     barrier()
     return job_elapsed(time.perf_counter() - t0, world), scan
+
+
+def static_leg(torch, buf, local, ks=(300000, 2000000), nbytes=1 << 30, reps=3):
+    """The static index at repository scale: the first GiB of
+    the stream against K random ids known by value only (ChunkIndex::loadIndex
+    of earlier backups' index files, chunk_index.cc:26-79), rolling-hash ids;
+    the best of `reps` whole zc_chunk_device calls after one warm-up."""
+    import numpy as np
+    from zbackup_amd import BackupCreator
+    out = {"unit": "GiB/s", "stream_bytes": nbytes, "chunk_max_size": W64,
+           "note": "two-level Bloom screen below 384 K ids, one-level with the in-kernel check table above (DESIGN 4.3)"}
+    for k in ks:
+        rng = np.random.default_rng(k)
+        keys = rng.integers(1, 2**63, k, dtype=np.int64).astype(np.uint64)
+        shas = rng.integers(0, 256, (k, 16), dtype=np.uint8)
+        with BackupCreator(W64, device=local, sha1=False, timing=True) as bc:
+            bc.seed_index_arrays(shas, keys, W64)
+            bc.chunk_device(buf.data_ptr(), nbytes)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                t1 = time.perf_counter()
+                bc.chunk_device(buf.data_ptr(), nbytes)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t1)
+            st = bc.stats()
+        out[f"ids_{k}"] = {"value": round(nbytes / min(ts) / 2**30, 2), "ms": round(min(ts) * 1e3, 3),
+                           "screen_ms": round(st["fscan_ms"], 3), "screen_runs": int(st["fscan_runs"])}
+    return out
 
 
 def bundle_leg(torch, buf, n, recs, world, local, cpu_sample):
@@ -572,6 +603,8 @@ def run_rank(args):
                     extras[key] = fb
         if args.config == "c2" and args.lzo:
             extras["bundle_lzo"] = bundle_leg(torch, buf, n, recs, world, local, rank == 0)
+        if args.config == "c2" and n >= 1 << 30:
+            extras["static_index"] = static_leg(torch, buf, local)
 
     cpu = None
     if not args.no_cpu_baseline and args.config == "c2":
@@ -650,6 +683,8 @@ def run_rank(args):
                 out[key] = extras[key]
         if "bundle_lzo" in extras:
             out["bundle_lzo"] = extras["bundle_lzo"]
+        if "static_index" in extras:
+            out["static_index"] = extras["static_index"]
         if cpu:
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

@@ -60,7 +60,17 @@ def test_large_static_index_device_vs_oracle(torch_cuda, nrand):
     want = oracle.chunk_array(data, W64, seeds=seeds)
     assert (want["kind"] == 1).sum() >= nreal
     t = torch_cuda.from_numpy(data).to("cuda")
-    with BackupCreator(W64, seeds=seeds, sha1=True) as bc:
+    if nrand >= 1000000:
+        # the random ids through the array form (seed_index_arrays), the
+        # stream's own ids as tuples
+        rng = np.random.default_rng(nrand)
+        keys = rng.integers(1, 2**63, nrand, dtype=np.int64)
+        shas = rng.integers(0, 256, (nrand, 16), dtype=np.uint8)
+        bc = BackupCreator(W64, seeds=seeds[:len(seeds) - nrand], sha1=True)
+        bc.seed_index_arrays(shas, keys.astype(np.uint64), W64)
+    else:
+        bc = BackupCreator(W64, seeds=seeds, sha1=True)
+    with bc:
         bc.chunk_device(t.data_ptr(), data.size)
         _same(bc.records(), want)
 

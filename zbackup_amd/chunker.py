@@ -88,6 +88,23 @@ class BackupCreator:
                 arr[i].size = size
             _check(self._L, self._ctx, self._L.zc_seed_index(self._ctx, arr, len(seeds)), "zc_seed_index")
 
+    def seed_index_arrays(self, sha1, rolling, size):
+        """seed_index for ids given as arrays: sha1 (n, 16) uint8, rolling (n,)
+        uint64, size a scalar or (n,) -- one copy into the ZcSeed array (an
+        index file's worth of ids without a Python loop)."""
+        rolling = np.ascontiguousarray(rolling, dtype=np.uint64)
+        n = rolling.size
+        if n == 0:
+            return
+        rec = np.zeros(n, dtype=np.dtype([("sha1", np.uint8, 16), ("rolling", np.uint64), ("size", np.uint32),
+                                          ("reserved", np.uint32)]))
+        assert rec.dtype.itemsize == ctypes.sizeof(_lib.ZcSeed)
+        rec["sha1"] = np.asarray(sha1, dtype=np.uint8).reshape(n, 16)
+        rec["rolling"] = rolling
+        rec["size"] = size
+        arr = (_lib.ZcSeed * n).from_buffer(rec)
+        _check(self._L, self._ctx, self._L.zc_seed_index(self._ctx, arr, n), "zc_seed_index")
+
     def _new_stream(self):
         # A fed stream's records are taken from the context as they are cut and
         # serialized right away, while their bytes are still in the feed window
