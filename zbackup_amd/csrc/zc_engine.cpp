@@ -1287,6 +1287,11 @@ class Resolver {
       // set up the side stream)
       HCK(hipEventRecord(c_.ev_idx, c_.stream));
       const uint64_t* tab = nref_ && anchors ? c_.tab.p : nullptr;
+      // ZC_FLAG_SHA1, speculative (spec_): equal-key grid pairs are joined
+      // before the probe (a no-op without pairs; the count is on the device),
+      // so the probe runs once, on the classes as joined
+      const bool early_join = spec_ && nref_ && pre_sha_n_;
+      if (early_join) HCK(launch_class_sha(nullptr, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
       if (anchors)
         HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
                          c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
@@ -1309,29 +1314,31 @@ class Resolver {
       if (nref_ && c_.h_cnt[CNT_SPAIRS]) {
         // ZC_FLAG_SHA1: equal-key grid chunks whose SHA-1 the side stream
         // computes are decided by key + SHA-1 prefix, as ChunkIndex::findChunk
-        // decides (chunk_index.cc:119-143) -- no byte comparison; the probe
-        // then runs again on the final classes.  Speculatively (spec_): joined
-        // now, the walk runs while the SHA-1 does, and finalize_records checks
-        // every such pair's prefixes once they are in (a pair that differs --
-        // equal 64-bit keys of different bytes -- redoes the stream without
-        // speculation: Respeculate); else after the SHA-1 kernel
+        // decides (chunk_index.cc:119-143) -- no byte comparison.
+        // Speculatively (early_join): joined before the probe, the walk runs
+        // while the SHA-1 does, and finalize_records checks every such pair's
+        // prefixes once they are in (a pair that differs -- equal 64-bit keys
+        // of different bytes -- redoes the stream without speculation:
+        // Respeculate); else joined after the SHA-1 kernel, and the probe runs
+        // again on the final classes
         const uint64_t nsp = c_.h_cnt[CNT_SPAIRS];
-        if (spec_) {
+        if (early_join) {
           c_.h_pairs.ensure(nsp);
           d2h(c_, c_.h_pairs.p, c_.cpairs.p + (nref_ - nsp), nsp);
+          sync(c_);
         } else {
           HCK(hipStreamWaitEvent(c_.stream, c_.ev_sha, 0));
+          HCK(launch_class_sha(c_.gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
+          if (anchors) {
+            HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
+            HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
+                             c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p,
+                             c_.cand.cap, c_.counters.p, c_.stream));
+          }
+          d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
+          sync(c_);
         }
-        HCK(launch_class_sha(spec_ ? nullptr : c_.gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
-        if (anchors) {
-          HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
-          HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
-                           c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap,
-                           c_.counters.p, c_.stream));
-        }
-        d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
-        sync(c_);
-        if (spec_)  // the pairs to check, as grid chunk numbers
+        if (early_join)  // the pairs to check, as grid chunk numbers
           for (uint64_t t = 0; t < nsp; ++t) {
             const uint2 pr = c_.h_pairs.p[t];
             spec_pairs_.push_back({ref_start(pr.x) / W_, ref_start(pr.y) / W_});
