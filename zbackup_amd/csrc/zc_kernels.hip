@@ -1969,22 +1969,26 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
       // for without draining that DMA); the per-piece pass below then reads
       // hit masks
       uint32_t xo[kFPieces][4], hm[kFPieces];
-#pragma unroll
-      for (int p = 0; p < kFPieces; ++p) {
+      // the out-bytes of piece p (b[p - W], zero before the stream)
+      auto out_piece = [&](int p, uint32_t (&o)[4]) {
         const uint64_t pp = ps + (uint64_t)r * ZC_FROUND + 16 * p;
         const uint4 vout = funnel16<Q>(p == 0 ? carry : vst[p - 1], vst[p], sbyte);
-        xo[p][0] = vout.x;
-        xo[p][1] = vout.y;
-        xo[p][2] = vout.z;
-        xo[p][3] = vout.w;
+        o[0] = vout.x;
+        o[1] = vout.y;
+        o[2] = vout.z;
+        o[3] = vout.w;
         if (head && pp < W) {
           const uint64_t z = (uint64_t)W - pp;
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
             const uint64_t lo = 4 * d;
-            xo[p][d] = z >= lo + 4 ? 0u : (z > lo ? xo[p][d] & (~0u << (8 * (z - lo))) : xo[p][d]);
+            o[d] = z >= lo + 4 ? 0u : (z > lo ? o[d] & (~0u << (8 * (z - lo))) : o[d]);
           }
         }
+      };
+      if constexpr (NF == 64) {
+#pragma unroll
+        for (int p = 0; p < kFPieces; ++p) out_piece(p, xo[p]);
       }
       if constexpr (NF == 64) {
         // two halves of two pieces: 32 gathers in flight per lane each.  A
@@ -2043,50 +2047,71 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
         // false hits) is a run the walk's exact key test drops.
         const uint2* const bl = (const uint2*)K.bloom;
         const uint32_t bsh = 32u - K.nk, csh = 32u - K.cbits;
-        // piece by piece (16 gathers in flight per lane, two waves per SIMD)
-#pragma unroll
-        for (int p = 0; p < kFPieces; ++p) {
-          uint2 bw[16];
-          uint32_t gs[16], cb[16];
+        // piece by piece (16 gathers in flight per lane, two waves per SIMD),
+        // pipelined: piece p + 1's filter gathers are issued behind piece p's
+        // check-table reads, so the check's round trip overlaps them
+        uint2 bw[2][16], ev[2][16];
+        uint32_t gs[2][16], cb[2][16], cw[2][8], hx[2];  // cw: the check words, two per register
+        auto gather = [&](int p) {  // the keys of piece p and their filter blocks
+          const int b = p & 1;
           const uint32_t xin[4] = {vin[p].x, vin[p].y, vin[p].z, vin[p].w};
+          uint32_t xp[4];
+          out_piece(p, xp);
 #pragma unroll
           for (int d = 0; d < 4; ++d)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xo[p][d] >> (8 * q)) & 0xFFu) * K.pw64;
+              V64 = V64 * 257u + ((xin[d] >> (8 * q)) & 0xFFu) - (uint64_t)((xp[d] >> (8 * q)) & 0xFFu) * K.pw64;
               const uint64_t key = V64 + K.pw64;
               const uint32_t hi = (uint32_t)((key * kGolden) >> 32);  // bloom_block, chk_bucket
-              gs[4 * d + q] = bloom_seed(key);
-              cb[4 * d + q] = hi >> csh;
-              bw[4 * d + q] = bl[hi >> bsh];
+              gs[b][4 * d + q] = bloom_seed(key);
+              cb[b][4 * d + q] = hi >> csh;
+              bw[b][4 * d + q] = bl[hi >> bsh];
             }
-          uint32_t hx = 0;
+        };
+        auto test = [&](int p) {  // the filter test, and the hits' check-table reads
+          const int b = p & 1;
+          uint32_t h = 0;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) hx |= bloom_test(bw[i].x, bw[i].y, gs[i]) << i;
-          uint2 ev[16];
-#pragma unroll
-          for (int i = 0; i < 16; ++i)
-            if ((hx >> i) & 1u) ev[i] = K.chk[cb[i]];
-          uint32_t slow = 0;
+          for (int i = 0; i < 16; ++i) h |= bloom_test(bw[b][i].x, bw[b][i].y, gs[b][i]) << i;
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            if ((hx >> i) & 1u) {
-              const uint32_t v = chk_match(ev[i], chk_word_of_seed(gs[i]));
-              if (v == 0) hx &= ~(1u << i);  // an empty slot: not in the set
+            if ((h >> i) & 1u) ev[b][i] = K.chk[cb[b][i]];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) cw[b][i] = chk_word_of_seed(gs[b][2 * i]) | chk_word_of_seed(gs[b][2 * i + 1]) << 16;
+          hx[b] = h;
+        };
+        auto check = [&](int p) {  // the check words: exact hits of piece p
+          const int b = p & 1;
+          uint32_t h = hx[b], slow = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((h >> i) & 1u) {
+              const uint32_t v = chk_match(ev[b][i], (cw[b][i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+              if (v == 0) h &= ~(1u << i);  // an empty slot: not in the set
               else if (v == 2) slow |= 1u << i;  // a full bucket without it
             }
           if (__builtin_expect(__ballot(slow != 0) != 0, 0)) {
 #pragma unroll
             for (int i = 0; i < 16; ++i)
               if ((slow >> i) & 1u) {
-                const uint32_t c = chk_word_of_seed(gs[i]);
-                uint32_t b = cb[i] + 1, v;
-                while ((v = chk_match(K.chk[b], c)) == 2) ++b;  // the last pad bucket ends every chain
-                if (v == 0) hx &= ~(1u << i);
+                const uint32_t c = (cw[b][i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                uint32_t k = cb[b][i] + 1, v;
+                while ((v = chk_match(K.chk[k], c)) == 2) ++k;  // the last pad bucket ends every chain
+                if (v == 0) h &= ~(1u << i);
               }
           }
-          hm[p] = hx;
+          hm[p] = h;
+        };
+        gather(0);
+        test(0);
+#pragma unroll
+        for (int p = 1; p < kFPieces; ++p) {
+          gather(p);
+          check(p - 1);
+          test(p);
         }
+        check(kFPieces - 1);
       }
       if (R + 2 < nR) issue(R + 2);
 #pragma unroll
