@@ -18,6 +18,9 @@ before anything touches a GPU, and exits with their status; under
 
 Besides the headline `value` (chunk ids = rolling hash, as BASELINE's metric
 names), the same line carries, driver-observed:
+  value_c3, value_c5
+               BASELINE configs[2] and [4] (C3: two copies of 4 GiB; C5: all
+               zeros) in the headline mode, timed as the headline
   value_sha1   the same streams with complete ChunkIds (SHA-1 prefix + rolling
                hash on every record: backup_creator.cc:130-131, chunk_id.cc:19-27)
   end_to_end   the stream starting in pinned host memory (zc_chunk_host: H2D
@@ -503,6 +506,30 @@ def run_rank(args):
     # to the headline, the per-GPU fractions and the concurrent CPU baseline, so
     # N ranks do not each pin 8 GiB of host memory for the end-to-end legs
     if not args.no_extras and world == 1:
+        # BASELINE configs[2] (C3, 50 % duplicated) and configs[4] (C5, all
+        # zeros) in the headline's own mode (rolling-hash ids), timed exactly as
+        # the headline: W untimed + K timed steps between barriers and syncs
+        if args.config == "c2" and not args.sha1:
+            other = torch.empty(n, dtype=torch.uint8, device=buf.device)
+            for cfg in ("c3", "c5"):
+                fill_stream(torch, other, n, cfg, seed, local)
+                bo = BackupCreator(W64, device=local, sha1=False, timing=True)
+
+                def step_cfg():
+                    bo.chunk_device(other.data_ptr(), n)
+                    return bo.scan_ms()
+
+                elo, scan_o = timed_steps(torch, world, step_cfg, args.warmup, args.steps)
+                sto = bo.stats()
+                nrec_o = len(bo.records())
+                bo.close()
+                extras[f"value_{cfg}"] = {"value": round(job_value(n, world, args.steps, elo), 3), "unit": "GiB/s",
+                                          "ms_per_step": round(elo / args.steps * 1e3, 3), "steps": args.steps,
+                                          "warmup": args.warmup, "workload": CONFIGS[cfg],
+                                          "chunks_per_s": round(nrec_o * args.steps / elo, 1),
+                                          "scan_ms_avg": round(sum(scan_o) / len(scan_o), 4),
+                                          "stages": stage_dict(sto)}
+            del other
         # complete ChunkIds on every record (the mode the zbackup binding runs,
         # integration/gpu_backup_creator.hh): C2, and C3 / C5 in a second buffer
         if not args.sha1 and args.sha1_steps > 0:
@@ -667,7 +694,7 @@ def run_rank(args):
             out["value_sha1"] = round(extras["value_sha1"], 3)
             out["sha1_ms_per_step"] = round(extras["sha1_ms_per_step"], 3)
             out["sha1_stages"] = extras["sha1_stages"]
-        for key in ("value_sha1_c3", "value_sha1_c5"):
+        for key in ("value_c3", "value_c5", "value_sha1_c3", "value_sha1_c5"):
             if key in extras:
                 out[key] = extras[key]
         for key in ("end_to_end", "end_to_end_sha1"):

@@ -9,6 +9,10 @@ hash in these files comes from the reference's code; the boundary rules come
 from the restatement (backup_creator.cc itself cannot be built here: it needs
 the generated zbackup.pb.h and the libprotobuf runtime, which the image lacks).
 
+`make_golden.py [OUTDIR]` writes into OUTDIR (default: this directory);
+tests/test_oracle_ref.py regenerates into a temporary directory and diffs the
+result against the committed files.
+
 Each case is a synthetic stream spec (grammar: oracle/zc_oracle.h), so the GPU
 box regenerates the exact bytes without /root/reference.  Fixture format:
   # key: value        header (case, spec, W, seed_spec)
@@ -69,13 +73,13 @@ def seeds_from(spec, W):
     return [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in recs if k == "N"]
 
 
-def main():
+def main(out_dir=HERE):
     oracle.build(ref=True)
     for name, spec, W, seed_spec in CASES:
         data = oracle.gen(spec, ref=True)
         seeds = seeds_from(seed_spec, W) if seed_spec else []
         recs = oracle.chunk(data, W, seeds=seeds, ref=True)
-        with open(os.path.join(HERE, f"{name}.txt"), "w") as f:
+        with open(os.path.join(out_dir, f"{name}.txt"), "w") as f:
             f.write(f"# case: {name}\n# spec: {spec}\n# W: {W}\n# n: {data.size}\n")
             f.write(f"# seed_spec: {seed_spec or '-'}\n")
             f.write("# generator: oracle/_ref (restated BackupCreator + reference rolling_hash.cc)\n")
@@ -86,7 +90,7 @@ def main():
         kinds = {c: sum(1 for r in recs if r[0] == c) for c in "NDB"}
         print(f"{name:22s} n={data.size:9d} W={W:6d} records={len(recs):6d} {kinds}")
     L = oracle.lib(ref=True)
-    with open(os.path.join(HERE, "kat_digest.txt"), "w") as f:
+    with open(os.path.join(out_dir, "kat_digest.txt"), "w") as f:
         f.write("# RollingHash::digest(buf, size) known answers, computed by the reference's\n")
         f.write("# rolling_hash.cc (oracle/_ref/liboracle_ref.so).  <name> <spec> <digest>\n")
         for name, spec in KAT_SPECS:
@@ -95,4 +99,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else HERE)

@@ -164,3 +164,35 @@ def test_historic_key_collision_and_seeded_wrong_prefix(torch_cuda, W):
                 bc.feed(b)
                 bc.finish()
             assert bc.record_tuples() == want_b, path
+
+
+@pytest.mark.parametrize("W", [4096, 65536])
+def test_respeculation_on_a_context_with_history_and_seeds(torch_cuda, W):
+    # a refuted speculative join (equal-key grid chunks C1, C2 of different
+    # bytes) redoes the stream after its historic registration has grown the
+    # device index: the redo must start from the index exactly as the stream
+    # found it -- earlier streams' historic entries and by-value seeds kept,
+    # nothing of the refuted pass left -- and the next stream must match the
+    # earlier streams' chunks, the redone stream's and the seeds (oracle)
+    from zbackup_amd import BackupCreator
+    c1, c2 = _tm_pair(W, 15)
+    a = _rand(6 * W + 77, 51)
+    s = _rand(3 * W, 52)
+    seeds = [(bytes(oracle.sha1(s[W:2 * W])[:16]), oracle.digest(s[W:2 * W]), W), (bytes(16 * [0x33]), 12345, W)]
+    b = np.concatenate([_rand(2 * W, 53), c1, c2, a[W:4 * W], _rand(W + 5, 54)])
+    d = np.concatenate([_rand(123, 55), a[2 * W:5 * W], c2, c1, s[W:2 * W], b[:2 * W], _rand(W, 56)])
+    index = list(seeds)
+    wants = []
+    for x in (a, b, d):
+        want = oracle.chunk(x, W, seeds=list(index))
+        index += [(bytes.fromhex(sha), h, sz) for (k, o, sz, h, sha) in want if k == "N" and sz == W]
+        wants.append(want)
+    assert sum(1 for r in wants[1] if r[0] == "D") >= 2
+    assert sum(1 for r in wants[2] if r[0] == "D") >= 6
+    with BackupCreator(W, seeds=seeds, sha1=True) as bc:
+        for i, (x, want) in enumerate(zip((a, b, d), wants)):
+            t = torch_cuda.from_numpy(np.ascontiguousarray(x)).to("cuda")
+            bc.chunk_device(t.data_ptr(), x.size)
+            assert bc.record_tuples() == want, i
+            assert bc.stats()["respeculations"] == (1 if i == 1 else 0), i
+            bc.reset()

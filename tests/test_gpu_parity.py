@@ -118,13 +118,13 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     assert _run_device(torch_cuda, data, W) == want
 
 
-# SHA-1 ids with the whole stream in one scan launch and at least one grid
-# chunk per scan lane (512 lanes per 2 MiB tile, one workgroup per CU up to 256):
-# the scan's lanes hash the grid chunks themselves (launch_scan_sha).  Cases:
-# a chunk ending in every round (W = 128), lanes with one chunk more than
-# others and more blocks than the rounds hold (the tail loop), W not a power of
-# two, a 3-byte partial last chunk, duplicates moving the grid, and 260 tiles
-# (workgroups with one and with two tiles)
+# SHA-1 ids on streams of many grid chunks per scan lane: the grid SHA-1
+# (zc_sha1_grid16_kernel, queued behind the first epoch's batch) hashes every
+# grid chunk, and records that are whole grid chunks take their prefix from
+# it.  Cases: many chunks per scan lane (W = 128), W not a power of two
+# (2944 = 16 * 184: the aligned kernel; the general one for W % 16 != 0 runs in
+# the fuzz suite), a 3-byte partial last chunk (zc_sha1_one_kernel),
+# duplicates moving the grid, and 260 scan tiles
 @pytest.mark.parametrize("W,spec", [
     (128, "R31:50000000,C7:3000000,R32:333"),
     (1024, "R33:40000000,Z:2000000,C123:5000000,R34:77777"),
@@ -132,10 +132,8 @@ def test_multi_tile_vs_oracle(torch_cuda, W):
     (4096, "R36:50343939"),
     (1024, "R37:545259520,R38:4321"),
 ])
-def test_fused_scan_sha1_vs_oracle(torch_cuda, W, spec):
+def test_grid_sha1_many_chunks_per_lane_vs_oracle(torch_cuda, W, spec):
     data = oracle.gen(spec)
-    ntiles = data.size // (2 << 20)
-    assert data.size // W >= min(ntiles, 256) * 512  # fusable on a 256-CU MI355X
     want = oracle.chunk(data, W)
     assert _run_device(torch_cuda, data, W) == want
 
@@ -425,3 +423,35 @@ def test_backup_data_of_a_long_windowed_stream(torch_cuda, sha1):
         assert bc.get_backup_data() == expect
         if sha1:
             assert bc.record_tuples() == want
+
+
+@pytest.mark.parametrize("path", ["device", "feed", "window"])
+def test_all_duplicate_middle_stream_keeps_the_index(torch_cuda, path):
+    # three (four) SHA-1 streams on one context: the second repeats the first,
+    # so it saves no W-byte chunk at all; the index the first stream built
+    # (keys and SHA-1 prefixes of its historic entries) must survive it, and
+    # must survive the third stream growing it, so the third and fourth
+    # streams match the first's chunks as ChunkIndex::findChunk would
+    # (chunk_index.cc:119-143 over the entries Writer::add registered)
+    from zbackup_amd import BackupCreator
+    a = oracle.gen("R701:700000")
+    b = oracle.gen("R702:33333,R701:700000,R703:150000")
+    d = oracle.gen("R704:999,R701:500000,R703:150000,R705:7")
+    index = []
+    wants = []
+    for s in (a, a, b, d):
+        want = oracle.chunk(s, W64, seeds=list(index))
+        index += [(bytes.fromhex(sha), h, sz) for (k, o, sz, h, sha) in want if k == "N" and sz == W64]
+        wants.append(want)
+    assert all(r[0] == "D" for r in wants[1] if r[2] == W64)
+    assert sum(1 for r in wants[2] if r[0] == "D") >= 8 and sum(1 for r in wants[3] if r[0] == "D") >= 6
+    with BackupCreator(W64, sha1=True, window=1 if path == "window" else None) as bc:
+        for s, want in zip((a, a, b, d), wants):
+            if path == "device":
+                t = torch_cuda.from_numpy(s).to("cuda")
+                bc.chunk_device(t.data_ptr(), s.size)
+            else:
+                bc.feed(s)
+                bc.finish()
+            assert bc.record_tuples() == want
+            bc.reset()

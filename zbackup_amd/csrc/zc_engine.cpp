@@ -305,8 +305,11 @@ class SpinTeam {
     std::lock_guard<std::mutex> one(run_);
     job_ = &f;
     n_ = n;
-    for (auto& c : claim_) c.store(0, std::memory_order_release);  // (job_, n_ published with it)
+    // done_ is cleared before any part can be claimed: a helper that claims a
+    // part of this job (the moment its claim word is reset) counts it after
+    // the clear, never into the previous job's count
     done_.store(0, std::memory_order_relaxed);
+    for (auto& c : claim_) c.store(0, std::memory_order_release);  // (job_, n_, done_ published with it)
     seq_.fetch_add(1, std::memory_order_release);
     int mine = 0;
     for (int k = 0; k < kParts; ++k)  // claim every part nobody took yet, from the last
@@ -340,7 +343,10 @@ class SpinTeam {
         cv_.wait(lk, [&] { return wake_ != woken; });
         woken = wake_;
       }
-      // spin until a job appears or the deadline passes
+      // spin until the deadline passes, taking this helper's part of every
+      // job started meanwhile (a sequence number seen before the wake-up is
+      // never taken for a new job: only a changed one is)
+      seen = seq_.load(std::memory_order_acquire);
       while (now_ns() < deadline_.load(std::memory_order_relaxed)) {
         const uint64_t s = seq_.load(std::memory_order_acquire);
         if (s != seen) {
@@ -349,7 +355,6 @@ class SpinTeam {
             part(w);
             done_.fetch_add(1, std::memory_order_release);
           }
-          break;
         }
         _mm_pause();
       }
@@ -1232,6 +1237,7 @@ class Resolver {
     f_min_vis_ = kInf;
     uint64_t ncand = 0, nancless = 0;
     const HistTab ht = hist_tab();
+    if (sha_behind_scan()) sha_launch();  // beside the batch, whose kernels take issue priority
     if (nref_ || ht.tab) {
       auto tm = Clock::now();
       EpochIndex ix{};
@@ -2331,6 +2337,16 @@ class Resolver {
   // 0.1).  After the batch the walk, the records and the index registration
   // run on the host while the SHA-1 does.
   bool sha_pending_ = false;
+  // ZC_SHA_AT=1 (A/B): the grid SHA-1 queued right behind the scan, beside
+  // the first epoch's batch (its latency-bound kernels run at wave priority 3,
+  // ZC_URGENT); 0: behind the batch
+  static bool sha_behind_scan() {
+    static const int v = [] {
+      const char* e = getenv("ZC_SHA_AT");
+      return e ? atoi(e) : 0;
+    }();
+    return v == 1;
+  }
   void pre_sha() {
     pre_sha_n_ = 0;
     gsha_ready_ = false;
@@ -2449,7 +2465,7 @@ class Resolver {
     // the stream's end straight into the historic index (their entries
     // hp.e0 + j), else kept with fresh_ until they join it
     uint8_t* fs;
-    const bool in_place = stream_end && f0 == 0 && hp.k == frec.size();
+    const bool in_place = stream_end && f0 == 0 && hp.k > 0 && hp.k == frec.size();
     if (in_place) {
       c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
       fs = c_.hsha.data() + 16 * (size_t)hp.e0;
@@ -2460,11 +2476,16 @@ class Resolver {
     auto fcopy = [&](size_t a, size_t b) {
       for (size_t j = a; j < b; ++j) memcpy(fs + 16 * j, rb[frec[j]].sha1, 16);
     };
+    const double t_fill = ms_since(tf);
     if (team && frec.size() >= kParallelRecordsMin) SpinTeam::get().run(frec.size(), fcopy);
     else fcopy(0, frec.size());
+    const double t_fcopy = ms_since(tf);
     c_.nrec_done = r1;
     if (stream_end) stream_end_index(&hp, in_place);
     c_.stats.sha_fill_ms += ms_since(tf);
+    if (getenv("ZC_DEBUG_FILL"))  // TEMP (round-5 measurement)
+      fprintf(stderr, "fill %.3f fcopy %.3f end %.3f (gq %zu frec %zu)\n", t_fill, t_fcopy - t_fill,
+              ms_since(tf) - t_fcopy, gq.size(), frec.size());
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the

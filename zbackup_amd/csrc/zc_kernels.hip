@@ -38,6 +38,16 @@ namespace {
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 typedef unsigned v2u32 __attribute__((ext_vector_type(2)));
 
+// Wave issue priority for the short, latency-bound kernels (chunk metadata,
+// index inserts, probe, class joins, historic registration, range digests).
+// With ZC_FLAG_SHA1 they run while the grid SHA-1 kernel holds every SIMD
+// (VALU-bound, 96 % busy): a SIMD issues to the highest-priority ready wave,
+// oldest first among equals, so without this a kernel dispatched after the
+// SHA-1 waves only got their stall cycles (chunk metadata 1.2 ms instead of
+// 25 us, zc_ref_meta 21-412 us).  s_setprio only changes the
+// arbitration order of this wave's instructions; it has no other effect.
+#define ZC_URGENT() __builtin_amdgcn_s_setprio(3)
+
 __host__ __device__ inline uint64_t pow257_dev(uint64_t e) {
   uint64_t r = 1, b = 257;
   while (e) {
@@ -866,6 +876,7 @@ __global__ void __launch_bounds__(ZC_WT_BLOCK) zc_anchor_rescan_kernel(const uin
 // entries [0, cnt) that point into the main pool follow their shares
 __global__ void zc_slide_dir_kernel(uint32_t* __restrict__ base, const uint32_t* __restrict__ dcnt, uint32_t cnt,
                                     uint32_t shift) {
+  ZC_URGENT();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < cnt && dcnt[i] != ZC_WT_OVERFLOW && !(base[i] & ZC_SIDE_POOL)) base[i] -= shift;
 }
@@ -973,6 +984,7 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
                                      uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
                                      uint32_t* __restrict__ anc_off, EpochClear ec) {
+  ZC_URGENT();
   const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
   if (ec.tab)
@@ -1001,6 +1013,7 @@ __global__ void zc_ref_meta_kernel(const uint8_t* __restrict__ data, const uint6
                                    const uint64_t* __restrict__ starts, uint32_t cnt, uint32_t W, uint64_t pw,
                                    uint64_t* __restrict__ key, uint32_t* __restrict__ anc_off,
                                    uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp) {
+  ZC_URGENT();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cnt) return;
   const uint64_t c = starts[i];
@@ -1021,6 +1034,7 @@ __global__ void zc_ref_gather_kernel(const uint32_t* __restrict__ src, const uin
                                      const uint32_t* __restrict__ cgv, const uint64_t* __restrict__ cfpv,
                                      uint64_t* __restrict__ key, uint32_t* __restrict__ anc, uint32_t* __restrict__ g,
                                      uint64_t* __restrict__ fp) {
+  ZC_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cnt) return;
   const uint32_t r = src[t], e = dst[t];
@@ -1157,6 +1171,7 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     const uint32_t* __restrict__ cls, const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r,
     uint64_t n, uint32_t W, HistTab ht, EpochGrid eg,
     Cand* __restrict__ cand, uint64_t cand_cap, unsigned long long* __restrict__ counters) {
+  ZC_URGENT();
   const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   constexpr int kS = kProbeWT * kProbeSlots;
@@ -1300,6 +1315,7 @@ __global__ void __launch_bounds__(256) zc_verify_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ ref_start,
                                                         uint32_t len, uint32_t npairs,
                                                         uint8_t* __restrict__ ok) {
+  ZC_URGENT();
   const uint32_t wave = (uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const uint32_t lane = threadIdx.x & 63;
   if (wave >= npairs) return;
@@ -1322,6 +1338,7 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
                                        const uint32_t* __restrict__ cg, const uint64_t* __restrict__ cfp,
                                        uint32_t nref, uint64_t* ckeys, uint32_t cbits,
                                        uint64_t* tab, uint32_t tbits, uint32_t* __restrict__ gfilt) {
+  ZC_URGENT();
   // threads [0, nref) insert into the class table, [nref, 2 nref) into the
   // anchor table: the two CAS chains run side by side
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1373,6 +1390,7 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
 __global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint64_t* __restrict__ fp,
                                       const uint32_t* __restrict__ anc, uint32_t e0, uint32_t cnt, uint64_t* tab,
                                       uint32_t bits, uint32_t* __restrict__ filt) {
+  ZC_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cnt) return;
   const uint32_t e = e0 + t, gv = g[e];
@@ -1403,6 +1421,7 @@ __global__ void __launch_bounds__(256) zc_class_lead_kernel(
     const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off, uint32_t nref,
     const uint64_t* __restrict__ ckeys, uint32_t cbits, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
     uint2* __restrict__ pairs, unsigned long long* __restrict__ counters, ShaGrid sg, const uint64_t* __restrict__ start) {
+  ZC_URGENT();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nref) return;
   const uint64_t k = key[i];
@@ -1437,6 +1456,7 @@ __global__ void __launch_bounds__(256) zc_class_sha_kernel(ShaGrid sg, const uin
                                                            uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless,
                                                            const uint2* __restrict__ pairs,
                                                            unsigned long long* __restrict__ counters) {
+  ZC_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = t < counters[CNT_SPAIRS];
   bool same = false;
@@ -1460,6 +1480,7 @@ __global__ void __launch_bounds__(256) zc_class_verify_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ start, const uint32_t* __restrict__ anc_off,
     uint32_t W, uint32_t* __restrict__ cls, uint32_t* __restrict__ ancless, const uint2* __restrict__ pairs,
     unsigned long long* __restrict__ counters) {
+  ZC_URGENT();
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t np = counters[CNT_PAIRS];
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -1485,6 +1506,7 @@ __global__ void zc_range_digest_kernel(const uint8_t* __restrict__ data, uint64_
                                        const uint64_t* __restrict__ blk, const uint64_t* __restrict__ a,
                                        const uint64_t* __restrict__ b, uint32_t nr,
                                        uint64_t* __restrict__ out) {
+  ZC_URGENT();
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nr) return;
   out[i] = pow257_dev(b[i] - a[i]) + rk_acc(data, blk, a[i], b[i]);
@@ -1499,6 +1521,7 @@ struct SmallRanges {
 __global__ void zc_range_digest_small_kernel(const uint8_t* __restrict__ data, uint64_t n,
                                              const uint64_t* __restrict__ blk, SmallRanges rg,
                                              uint64_t* __restrict__ out) {
+  ZC_URGENT();
   const uint32_t i = threadIdx.x;
   if (i < rg.nr) out[i] = pow257_dev(rg.b[i] - rg.a[i]) + rk_acc(data, blk, rg.a[i], rg.b[i]);
 }
@@ -2289,6 +2312,7 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
 // Bloom filter of a key set (thread per key)
 __global__ void zc_bloom_add_kernel(uint32_t* __restrict__ bloom, uint32_t bits, const uint64_t* __restrict__ keys,
                                     uint32_t n) {
+  ZC_URGENT();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t b = bloom_block(keys[i], bits), g = bloom_seed(keys[i]);
@@ -2333,6 +2357,7 @@ __global__ void zc_key64_filter_kernel(const uint8_t* __restrict__ data, const u
                                        uint64_t pw, Run* __restrict__ runs, uint64_t nruns,
                                        const uint64_t* __restrict__ set, uint32_t sbits, int zero_key,
                                        const uint64_t* __restrict__ list, uint32_t nl) {
+  ZC_URGENT();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nruns) return;
   const Run r = runs[i];
@@ -2857,6 +2882,7 @@ hipError_t launch_bloom_add(uint32_t* bloom, uint32_t bits, const uint64_t* keys
 // present already, or the table's end reached: done (the latter flagged)
 __global__ void zc_chk_add_kernel(uint16_t* __restrict__ chk, uint32_t bits, const uint64_t* __restrict__ keys,
                                   uint32_t n, unsigned int* __restrict__ ovf) {
+  ZC_URGENT();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t c = chk_word(keys[i]);
