@@ -237,9 +237,17 @@ def fill_stream(torch, buf, n, config, seed, local):
     torch.cuda.synchronize()
 
 
-def timed_steps(torch, world, step, warmup, steps):
-    """W untimed steps, then K timed steps between barriers + device syncs;
-    returns (job time = max over ranks, per-step scan ms of this rank)."""
+# Untimed warm-up: at least W steps and at least this long.  The GPU takes
+# ~10-20 ms of sustained load to reach its steady clock: in a kernel trace of
+# the headline (round 4, 1.9 ms steps) the scan ran 1.86-1.91 ms for the
+# first launches and settled at 1.53-1.58 ms from the eighth on.
+MIN_WARMUP_S = 0.25
+
+
+def timed_steps(torch, world, step, warmup, steps, min_warmup_s=MIN_WARMUP_S):
+    """W untimed steps (repeated until min_warmup_s has passed), then K timed
+    steps between barriers + device syncs; returns (job time = max over ranks,
+    per-step scan ms of this rank)."""
     import torch.distributed as dist
 
     def barrier():
@@ -247,8 +255,15 @@ def timed_steps(torch, world, step, warmup, steps):
         if world > 1:
             dist.barrier()
 
+    t_w = time.perf_counter()
     for _ in range(warmup):
         step()
+    if warmup > 0:
+        while True:
+            torch.cuda.synchronize()
+            if time.perf_counter() - t_w >= min_warmup_s:
+                break
+            step()
     barrier()
     t0 = time.perf_counter()
     scan = [step() for _ in range(steps)]

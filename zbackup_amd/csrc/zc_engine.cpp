@@ -466,7 +466,7 @@ struct zc_ctx {
   // historic index: this context's W-byte chunks whose bytes are gone from HBM
   // (earlier streams, or evicted from the window), each with its first anchor
   std::vector<uint64_t> hkey;
-  std::vector<uint8_t> hsha;  // 16 bytes per entry
+  std::vector<uint8_t, DefaultInit<uint8_t>> hsha;  // 16 bytes per entry (resize leaves them to be written)
   uint32_t nhist = 0;
   DevBuf<uint32_t> hanc, hg;
   DevBuf<uint64_t> hfp, htab;
@@ -2374,7 +2374,7 @@ class Resolver {
   // Records [nrec_done, size) are complete once their pieces have digests
   // and (ZC_FLAG_SHA1) every chunk record its SHA-1 prefix.
   std::vector<uint64_t> fresh_;  // NEW W-byte chunks of the stream still resident: offset,
-  std::vector<uint8_t> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
+  std::vector<uint8_t, DefaultInit<uint8_t>> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
   // stream_end: the stream's end (run_final): with ZC_FLAG_SHA1 its new W-byte
   // chunks join the context's index here, their device metadata queued before
   // the wait for the grid SHA-1, so that wait ends the call with little after it
@@ -2421,21 +2421,29 @@ class Resolver {
     std::vector<uint32_t> sl;
     std::vector<size_t> idx;
     std::vector<uint64_t> gq;    // grid-chunk records: record index << 32 | chunk (both < 2^32)
+    std::vector<uint32_t> gslot;  // per gq entry: its fresh_ entry (from f0), or kNoSlot
     std::vector<uint32_t> frec;  // record (from r0) of each new fresh_ entry
+    std::vector<uint32_t> fsh;   // fresh_ entries (from f0) hashed here (not grid chunks): their idx entry
+    constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     const size_t f0 = fresh_.size();
     gq.reserve(r1 - r0);
+    gslot.reserve(r1 - r0);
     for (size_t i = r0; i < r1; ++i) {
       const zc_record& r = c_.recs[i];
       if (r.kind == ZC_BYTES) continue;
+      uint32_t slot = kNoSlot;
       if (r.kind == ZC_CHUNK_NEW && r.size == W_) {
+        slot = (uint32_t)frec.size();
         fresh_.push_back(r.offset);
         frec.push_back((uint32_t)(i - r0));
       }
       const uint64_t q = grid_q(r);
       if (q != kInf) {
         gq.push_back((uint64_t)(i - r0) << 32 | q);
+        gslot.push_back(slot);
         continue;
       }
+      if (slot != kNoSlot) fsh.push_back((uint32_t)idx.size());
       sa.push_back(r.offset);
       sl.push_back(r.size);
       idx.push_back(i);
@@ -2445,6 +2453,19 @@ class Resolver {
     auto th = Clock::now();
     if (stream_end) hp = hist_add_meta(fresh_);
     c_.stats.hist_ms += ms_since(th);
+    // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_: at
+    // the stream's end straight into the historic index (their entries
+    // hp.e0 + j), else kept with fresh_ until they join it.  Sized before
+    // the wait (no value-initialisation: every byte is written below).
+    uint8_t* fs;
+    const bool in_place = stream_end && f0 == 0 && hp.k > 0 && hp.k == frec.size();
+    if (in_place) {
+      c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
+      fs = c_.hsha.data() + 16 * (size_t)hp.e0;
+    } else {
+      fresh_sha_.resize(16 * fresh_.size());
+      fs = fresh_sha_.data() + 16 * f0;
+    }
     const bool team = gq.size() >= kParallelRecordsMin;
     if (team) SpinTeam::get().arm();  // awake by the time the digests land
     auto tw = Clock::now();
@@ -2455,37 +2476,34 @@ class Resolver {
     spec_pairs_.clear();
     auto tf = Clock::now();
     zc_record* const rb = c_.recs.data() + r0;
+    // one pass: each grid-chunk record's prefix from the side stream's
+    // digests, into the record and, for a new chunk, its index slot; the
+    // record lines are fetched for writing a few entries ahead
     auto fill = [&](size_t a, size_t b) {
-      for (size_t j = a; j < b; ++j) memcpy(rb[gq[j] >> 32].sha1, gsha + 20 * (uint32_t)gq[j], 16);
+      constexpr size_t kAhead = 8;
+      for (size_t j = a; j < std::min(b, a + kAhead); ++j) __builtin_prefetch(rb[gq[j] >> 32].sha1, 1);
+      for (size_t j = a; j < b; ++j) {
+        if (j + kAhead < b) __builtin_prefetch(rb[gq[j + kAhead] >> 32].sha1, 1);
+        const uint8_t* src = gsha + 20 * (uint32_t)gq[j];
+        memcpy(rb[gq[j] >> 32].sha1, src, 16);
+        if (gslot[j] != kNoSlot) memcpy(fs + 16 * (size_t)gslot[j], src, 16);
+      }
     };
     if (team) SpinTeam::get().run(gq.size(), fill);
     else fill(0, gq.size());
     for (size_t j = 0; j < idx.size(); ++j) memcpy(c_.recs[idx[j]].sha1, &sh[j * 20], 16);
-    // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_: at
-    // the stream's end straight into the historic index (their entries
-    // hp.e0 + j), else kept with fresh_ until they join it
-    uint8_t* fs;
-    const bool in_place = stream_end && f0 == 0 && hp.k > 0 && hp.k == frec.size();
-    if (in_place) {
-      c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
-      fs = c_.hsha.data() + 16 * (size_t)hp.e0;
-    } else {
-      fresh_sha_.resize(16 * fresh_.size());
-      fs = fresh_sha_.data() + 16 * f0;
+    for (uint32_t t : fsh) {  // new chunks hashed here: their slot is their place among frec
+      const uint32_t rec = (uint32_t)(idx[t] - r0);
+      const size_t slot = std::lower_bound(frec.begin(), frec.end(), rec) - frec.begin();
+      memcpy(fs + 16 * slot, &sh[t * 20], 16);
     }
-    auto fcopy = [&](size_t a, size_t b) {
-      for (size_t j = a; j < b; ++j) memcpy(fs + 16 * j, rb[frec[j]].sha1, 16);
-    };
     const double t_fill = ms_since(tf);
-    if (team && frec.size() >= kParallelRecordsMin) SpinTeam::get().run(frec.size(), fcopy);
-    else fcopy(0, frec.size());
-    const double t_fcopy = ms_since(tf);
     c_.nrec_done = r1;
     if (stream_end) stream_end_index(&hp, in_place);
     c_.stats.sha_fill_ms += ms_since(tf);
     if (getenv("ZC_DEBUG_FILL"))  // TEMP (round-5 measurement)
-      fprintf(stderr, "fill %.3f fcopy %.3f end %.3f (gq %zu frec %zu)\n", t_fill, t_fcopy - t_fill,
-              ms_since(tf) - t_fcopy, gq.size(), frec.size());
+      fprintf(stderr, "fill %.3f end %.3f (gq %zu frec %zu)\n", t_fill, ms_since(tf) - t_fill, gq.size(),
+              frec.size());
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
