@@ -195,6 +195,35 @@ __global__ void __launch_bounds__(512, 1) rs_scan_kernel(const uint8_t* __restri
   }
 }
 
+// reads only (no hashing): the prototype's load pattern (lane: 64 bytes of
+// each 4 KiB row, four 16-byte loads) against fully coalesced rows (lane: 16
+// bytes of each 1 KiB row), same depth, the XOR of everything kept live
+template <int kLaneB>
+__global__ void __launch_bounds__(512, 1) rs_loads_kernel(const uint8_t* __restrict__ data, uint64_t nwt,
+                                                          uint32_t* __restrict__ sink) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  constexpr int kRowB = 64 * kLaneB, kLoads = kLaneB / 16, kRows = (64 * ZC_LSPAN) / kRowB;
+  uint32_t acc = 0;
+  for (uint64_t wt = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; wt < nwt; wt += waves) {
+    const uint8_t* base = data + (wt << ZC_WT_SHIFT) + lane * kLaneB;
+#pragma unroll 1
+    for (int r = 0; r < kRows; r += 4) {
+      v4u32 v[4][kLoads];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < kLoads; ++j) v[u][j] = ldnt(base + (uint64_t)(r + u) * kRowB + 16 * j);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < kLoads; ++j) acc ^= v[u][j][0] ^ v[u][j][1] ^ v[u][j][2] ^ v[u][j][3];
+    }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 }  // namespace rs
 
 int main(int argc, char** argv) {
@@ -256,7 +285,7 @@ int main(int argc, char** argv) {
   printf("span digests differing: %llu of %zu; wave-tiles with other anchor counts: %llu of %llu (%llu anchors)\n",
          (unsigned long long)dig_diff, ha.size(), (unsigned long long)cnt_diff, (unsigned long long)nwt,
          (unsigned long long)anc);
-  std::vector<float> t[3];
+  std::vector<float> t[5];
   for (int r = 0; r < rounds; ++r)
     for (int v = 0; v < 3; ++v) {
       float ms;
@@ -268,9 +297,21 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, a, b));
       if (r) t[v].push_back(ms);
     }
-  const char* names[3] = {"shipped zc_scan_kernel (LDS ring)", "register-staged, 2 waves/SIMD",
-                          "register-staged, 4 waves/SIMD"};
-  for (int v = 0; v < 3; ++v) {
+  const char* names[5] = {"shipped zc_scan_kernel (LDS ring)", "register-staged, 2 waves/SIMD",
+                          "register-staged, 4 waves/SIMD", "loads only, 64 B per lane per row",
+                          "loads only, 16 B per lane per row"};
+  for (int r = 0; r < rounds; ++r)
+    for (int v = 3; v < 5; ++v) {
+      float ms;
+      CK(hipEventRecord(a));
+      if (v == 3) hipLaunchKernelGGL(rs::rs_loads_kernel<64>, dim3(cus), dim3(512), 0, 0, d, nwt, rcnt);
+      else hipLaunchKernelGGL(rs::rs_loads_kernel<16>, dim3(cus), dim3(512), 0, 0, d, nwt, rcnt);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      CK(hipEventElapsedTime(&ms, a, b));
+      if (r) t[v].push_back(ms);
+    }
+  for (int v = 0; v < 5; ++v) {
     std::sort(t[v].begin(), t[v].end());
     printf("%-36s median %.3f ms  min %.3f ms  %.1f GB/s\n", names[v], t[v][t[v].size() / 2], t[v][0],
            n / (t[v][t[v].size() / 2] * 1e6));

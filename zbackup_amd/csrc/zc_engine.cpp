@@ -271,7 +271,7 @@ class HostPool {
   bool stop_ = false;
 };
 
-// Three helper threads for a short job that follows a wait: arm() wakes them
+// Seven helper threads for a short job that follows a wait: arm() wakes them
 // before the wait (a sleeping thread's wake-up costs more than the job
 // itself: the records' SHA-1 fill took 0.4-1.0 ms on the host pool against
 // 0.2 ms on one thread), they spin until run() hands them their parts (or
@@ -322,7 +322,7 @@ class SpinTeam {
   }
 
  private:
-  static constexpr int kHelpers = 3, kParts = kHelpers + 1;
+  static constexpr int kHelpers = 7, kParts = kHelpers + 1;
   static int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
@@ -2479,15 +2479,23 @@ class Resolver {
     // one pass: each grid-chunk record's prefix from the side stream's
     // digests, into the record and, for a new chunk, its index slot; the
     // record lines are fetched for writing a few entries ahead
+    // (the index slots are written past the caches: nothing reads them soon)
+    const bool fs_nt = ((uintptr_t)fs & 15) == 0;
     auto fill = [&](size_t a, size_t b) {
-      constexpr size_t kAhead = 8;
+      constexpr size_t kAhead = 32;
       for (size_t j = a; j < std::min(b, a + kAhead); ++j) __builtin_prefetch(rb[gq[j] >> 32].sha1, 1);
       for (size_t j = a; j < b; ++j) {
         if (j + kAhead < b) __builtin_prefetch(rb[gq[j + kAhead] >> 32].sha1, 1);
         const uint8_t* src = gsha + 20 * (uint32_t)gq[j];
-        memcpy(rb[gq[j] >> 32].sha1, src, 16);
-        if (gslot[j] != kNoSlot) memcpy(fs + 16 * (size_t)gslot[j], src, 16);
+        const __m128i v = _mm_loadu_si128((const __m128i*)src);
+        _mm_storeu_si128((__m128i*)rb[gq[j] >> 32].sha1, v);
+        if (gslot[j] != kNoSlot) {
+          uint8_t* d = fs + 16 * (size_t)gslot[j];
+          if (fs_nt) _mm_stream_si128((__m128i*)d, v);
+          else _mm_storeu_si128((__m128i*)d, v);
+        }
       }
+      _mm_sfence();
     };
     if (team) SpinTeam::get().run(gq.size(), fill);
     else fill(0, gq.size());
