@@ -1,7 +1,9 @@
-// Ablation timing of zc_scan_kernel variants (ablation bits in zc_kernels.hip),
-// interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
-// Tooling only.  Build: hipcc -O3 --offload-arch=gfx950 -I../../zbackup_amd/csrc scan_ablate.hip
+// Ablation timing of scan variants (the ABL_* bits of scan_ablate_kernel.hip)
+// against the product zc_scan_kernel, interleaved rounds in one process
+// (cdna_hip_programming.md §5.4 rule 24).  Tooling only.
+// Build: hipcc -O3 --offload-arch=gfx950 -I../../zbackup_amd/csrc scan_ablate.hip
 #include "../../zbackup_amd/csrc/zc_kernels.hip"
+#include "scan_ablate_kernel.hip"
 
 #include <cstdio>
 #include <vector>
@@ -23,13 +25,14 @@ int main(int argc, char** argv) {
   const PoolOut po{dbase, dcnt, prel, pg, wcap, 0};
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
-  constexpr int P = kScanProduct;
+  constexpr int P = kAblProduct;
   std::vector<V> vs = {
-    {"product (nt DMA)", zc_scan_kernel<P>, {}},
-    {"no_atomic", zc_scan_kernel<P | ABL_NO_ATOMIC>, {}},
-    {"te_no_anchor_store", zc_scan_kernel<P | ABL_TE_NO_ANCHOR_STORE>, {}},
-    {"te_digest_only", zc_scan_kernel<P | ABL_TE_DIGEST_ONLY>, {}},
-    {"te_no_store", zc_scan_kernel<P | ABL_TE_NO_STORE>, {}},
+    {"product zc_scan_kernel", zc_scan_kernel, {}},
+    {"ablation copy, product bits", abl_scan_kernel<P>, {}},
+    {"no_atomic", abl_scan_kernel<P | ABL_NO_ATOMIC>, {}},
+    {"te_no_anchor_store", abl_scan_kernel<P | ABL_TE_NO_ANCHOR_STORE>, {}},
+    {"te_digest_only", abl_scan_kernel<P | ABL_TE_DIGEST_ONLY>, {}},
+    {"te_no_store", abl_scan_kernel<P | ABL_TE_NO_STORE>, {}},
   };
   for (int round = 0; round < 25; ++round)
     for (auto& v : vs) {

@@ -189,87 +189,12 @@ struct DefaultInit : std::allocator<T> {
   }
 };
 
-// A few host threads for the record writing of long grid runs (a stream's
-// records are ~40 bytes each, 131,072 per 8 GiB: one core writes them at its
-// store bandwidth).  Workers sleep between jobs; the caller takes a share.
+// The record writes of long grid runs (a stream's records are ~40 bytes each,
+// 131,072 per 8 GiB: one core writes them at its store bandwidth) are split
+// over the spinning team below.
 static_assert(sizeof(zc_record) == 40 && offsetof(zc_record, size) == 8 && offsetof(zc_record, kind) == 12 &&
                   offsetof(zc_record, rolling) == 16 && offsetof(zc_record, sha1) == 24,
               "the streamed record writes assume this layout");
-
-class HostPool {
- public:
-  static HostPool& get() {
-    // one pool per process: a forked child gets its own (the parent's
-    // workers do not exist there); the old one is left as it is
-    static std::mutex mk;
-    static HostPool* pool = nullptr;
-    static pid_t owner = 0;
-    std::lock_guard<std::mutex> lk(mk);
-    if (!pool || owner != getpid()) {
-      pool = new HostPool;
-      owner = getpid();
-    }
-    return *pool;
-  }
-  // f(begin, end) over [0, n) in kParts contiguous parts
-  void run(size_t n, const std::function<void(size_t, size_t)>& f) {
-    std::lock_guard<std::mutex> one(run_);  // one job at a time (contexts may share the pool)
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      job_ = &f;
-      n_ = n;
-      pending_ = kWorkers;
-      ++gen_;
-    }
-    cv_.notify_all();
-    part(0, n, f);
-    std::unique_lock<std::mutex> lk(m_);
-    done_.wait(lk, [&] { return pending_ == 0; });
-    job_ = nullptr;
-  }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      stop_ = true;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-
- private:
-  static constexpr int kWorkers = 3, kParts = kWorkers + 1;  // 7 measured no faster
-  HostPool() {
-    for (int w = 0; w < kWorkers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
-  }
-  static void part(int k, size_t n, const std::function<void(size_t, size_t)>& f) {
-    const size_t a = n * k / kParts, b = n * (k + 1) / kParts;
-    if (b > a) f(a, b);
-  }
-  void loop(int k) {
-    uint64_t seen = 0;
-    for (;;) {
-      std::unique_lock<std::mutex> lk(m_);
-      cv_.wait(lk, [&] { return gen_ != seen; });
-      seen = gen_;
-      if (stop_) return;
-      const auto* f = job_;
-      const size_t n = n_;
-      lk.unlock();
-      part(k, n, *f);
-      lk.lock();
-      if (--pending_ == 0) done_.notify_one();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex run_, m_;
-  std::condition_variable cv_, done_;
-  const std::function<void(size_t, size_t)>* job_ = nullptr;
-  size_t n_ = 0;
-  int pending_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
 
 // Seven helper threads for a short job that follows a wait: arm() wakes them
 // before the wait (a sleeping thread's wake-up costs more than the job
@@ -405,7 +330,7 @@ void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uin
     for (; j < b; ++j) put(j);
     _mm_sfence();
   };
-  if (n >= kParallelRecordsMin) HostPool::get().run(n, fill);
+  if (n >= kParallelRecordsMin) SpinTeam::get().run(n, fill);  // (armed by the epoch before its wait)
   else fill(0, n);
 }
 
@@ -1279,7 +1204,7 @@ class Resolver {
                         c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
-                        pre_sha_n_ ? c_.gsha.p : nullptr, pre_sha_n_};
+                        pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_};
         HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
@@ -1308,6 +1233,9 @@ class Resolver {
         HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c_.copy_stream));
       predict_tail();
+      // the walk writes this many grid records at once: have the record team
+      // spinning by the time the batch is in
+      if (nsref >= kParallelRecordsMin) SpinTeam::get().arm();
       const bool first = !scan_checked_ && meta_from_scan_;  // this batch also waits for the scan
       if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
@@ -1334,7 +1262,7 @@ class Resolver {
           sync(c_);
         } else {
           HCK(hipStreamWaitEvent(c_.stream, c_.ev_sha, 0));
-          HCK(launch_class_sha(c_.gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
+          HCK(launch_class_sha(c_.h_gsha.p, pre_sha_n_, n_, W_, ix, nref_, c_.stream));
           if (anchors) {
             HCK(hipMemsetAsync(c_.counters.p + CNT_CAND, 0, sizeof(unsigned long long), c_.stream));
             HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
@@ -2354,7 +2282,6 @@ class Resolver {
     if (!(c_.flags & ZC_FLAG_SHA1) || !indexable_ || n_ < W_) return;
     const uint64_t k = (n_ + W_ - 1) / W_;
     if (k > 0xFFFFFFFFull) return;
-    c_.gsha.ensure(k * 20);
     c_.h_gsha.ensure(k * 20);
     pre_sha_n_ = k;
     sha_pending_ = true;
@@ -2365,9 +2292,11 @@ class Resolver {
     const uint64_t k = pre_sha_n_;
     HCK(hipEventRecord(c_.ev_sha, c_.stream));  // behind the batch (and the scan)
     HCK(hipStreamWaitEvent(c_.sha_stream, c_.ev_sha, 0));
-    HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.gsha.p, c_.sha_stream));
+    // the digests go straight to pinned host memory (dword stores from the
+    // kernel's lanes as they finish): no copy behind the kernel; the few
+    // device reads of them (class joins after the kernel) cross the bus
+    HCK(launch_sha1_grid(d_, n_, W_, (uint32_t)k, c_.h_gsha.p, c_.sha_stream));
     HCK(hipEventRecord(c_.ev_sha, c_.sha_stream));
-    HCK(hipMemcpyAsync(c_.h_gsha.p, c_.gsha.p, k * 20, hipMemcpyDeviceToHost, c_.sha_stream));
   }
 
   // ---------------------------------------------------------------- finalize

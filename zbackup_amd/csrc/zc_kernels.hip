@@ -205,22 +205,11 @@ __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
   return ((uint64_t)load4_any(data, q - 3) << 32) | load4_any(data, q - 7);
 }
 
-// Ablation bits (tools/ubench/scan_ablate.hip only; the product uses 0):
-// 1 = no digest, 2 = no gear/anchors, 4 = anchors counted but not recorded,
-// 8 = skip the per-byte work entirely (staging + reads only),
-// 16 = gear + max computed but folded into the state without a ballot/branch,
-// 32 = anchor threshold raised so the recording block is (almost) never taken,
-// 64 = no tile-end work (span digests, anchors to the pool), 128 = no
-// counter atomic, 256 = the tile end stores the span digests only
-enum { ABL_NO_DIGEST = 1, ABL_NO_GEAR = 2, ABL_NO_RECORD = 4, ABL_NO_BYTES = 8, ABL_NO_BRANCH = 16,
-       ABL_NEVER = 32, ABL_NO_TILE_END = 64, ABL_NO_ATOMIC = 128, ABL_TE_DIGEST_ONLY = 256,
-       ABL_DMA_NT = 512, ABL_DMA_SC1 = 1024, ABL_STAGGER_HALF = 2048, ABL_STAGGER_QUARTER = 4096,
-       ABL_NO_WARM = 8192, ABL_TE_NO_STORE = 16384, ABL_TE_NO_ANCHOR_STORE = 32768,
-       ABL_TE_DIGEST_NT = 65536, ABL_TE_DIGEST_SAME = 131072, ABL_PRIO = 262144,
-       ABL_DWORD_SAMPLED = 524288 /* timing only: anchors tested at dword ends only (experiment 16) */ };
-// the product's scan: the staging DMA is non-temporal (the stream is read
-// once; tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB)
-constexpr int kScanProduct = ABL_DMA_NT;
+// The staging DMA's cache policy: non-temporal (the stream is read once;
+// interleaved A/B in tools/ubench/scan_ablate.hip: 1.675 -> 1.560 ms per 8 GiB).
+// The ablation switches the round-4 scan carried (DESIGN 4.1's experiments)
+// live in tools/ubench/scan_ablate_kernel.hip, not in the product.
+constexpr int kScanDmaAux = 2;  // buffer_load ... lds, nt
 
 struct WaveList {   // per-wave LDS list of pieces holding anchors
   uint32_t* e;      // {the lane's previous entry | (rel of the piece >> 4) << 8 | lane << 16, gear before
@@ -244,71 +233,48 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 // anchor rate: each lane with a hit appends the piece (its bytes, the gear
 // before it and a link to the lane's previous entry) to the wave's LDS list,
 // and the tile end re-derives the exact anchors from those 16 bytes.
-// (ABL_DWORD_SAMPLED, timing only: the gear tested at dword ends alone -- a
-// quarter of the positions -- saves 6 % of the kernel, but windows at other
-// alignments then need every chunk's anchors in four residues, whose search
-// costs more than that: DESIGN 4.1, experiment 16.)
-template <int ABL>
+// (Anchors tested at dword ends alone -- a quarter of the positions -- save
+// 6 % of the kernel, but windows at other alignments then need every chunk's
+// anchors in four residues, whose search costs more than that: DESIGN 4.1,
+// experiment 16.)
 __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr, ScanLane& s, WaveList& wl,
                                            uint32_t& last) {
   const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-  if (ABL & ABL_NO_BYTES) {
-    s.hlo ^= xs[0] ^ xs[1] ^ xs[2] ^ xs[3];
-    return;
-  }
   const uint32_t g0 = s.glo;  // gear before the piece
   uint32_t g[4][4];
   int32_t mx[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t x = xs[d];
-    if ((ABL & ABL_DWORD_SAMPLED) && !(ABL & ABL_NO_GEAR)) {
-      s.glo = (s.glo << 4) + __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false);
-      mx[d] = d == 0 ? (int32_t)s.glo : max(mx[d - 1], (int32_t)s.glo);
-      g[d][3] = s.glo;
-    } else if (!(ABL & ABL_NO_GEAR)) {
-      const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
-                              __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
-                              __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
+    const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
+                            __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
+                            __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) g[d][k] = (s.glo << (k + 1)) + dd[k];
-      s.glo = g[d][3];
-      // one max3 chain over the piece's 16 gears (8 v_max3_i32 per piece)
-      mx[d] = d == 0 ? max(max((int32_t)g[0][0], (int32_t)g[0][1]), (int32_t)g[0][2])
-                     : max(max(mx[d - 1], (int32_t)g[d - 1][3]), (int32_t)g[d][0]);
-      if (d > 0) mx[d] = max(max(mx[d], (int32_t)g[d][1]), (int32_t)g[d][2]);
-    }
-    if (!(ABL & ABL_NO_DIGEST)) {
-      // two bytes per Horner step: acc*257^2 + (257 b_0 + b_1).  One v_perm
-      // swaps the bytes of each half (b_1 | b_0 << 8), an SDWA add adds b_0;
-      // acc*66049 + t is a v_mad_u64_u32 on the low word and one on the
-      // high word: 9 lane-ops per dword instead of 12
-      const uint32_t sp = __builtin_amdgcn_perm(0u, x, 0x02030001u);
-      const uint32_t t[2] = {(sp & 0xFFFFu) + (x & 0xFFu), (sp >> 16) + ((x >> 16) & 0xFFu)};
+    for (int k = 0; k < 4; ++k) g[d][k] = (s.glo << (k + 1)) + dd[k];
+    s.glo = g[d][3];
+    // one max3 chain over the piece's 16 gears (8 v_max3_i32 per piece)
+    mx[d] = d == 0 ? max(max((int32_t)g[0][0], (int32_t)g[0][1]), (int32_t)g[0][2])
+                   : max(max(mx[d - 1], (int32_t)g[d - 1][3]), (int32_t)g[d][0]);
+    if (d > 0) mx[d] = max(max(mx[d], (int32_t)g[d][1]), (int32_t)g[d][2]);
+    // two bytes per Horner step: acc*257^2 + (257 b_0 + b_1).  One v_perm
+    // swaps the bytes of each half (b_1 | b_0 << 8), an SDWA add adds b_0;
+    // acc*66049 + t is a v_mad_u64_u32 on the low word and one on the
+    // high word: 9 lane-ops per dword instead of 12
+    const uint32_t sp = __builtin_amdgcn_perm(0u, x, 0x02030001u);
+    const uint32_t t[2] = {(sp & 0xFFFFu) + (x & 0xFFu), (sp >> 16) + ((x >> 16) & 0xFFu)};
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        // acc*66049 + t = lo*66049 + {t, hi*66049}: a v_mul_lo_u32 for the
-        // high word feeds the 64-bit addend of ONE v_mad_u64_u32
-        const v2u32 addend = {t[k], s.hhi * 66049u};
-        const uint64_t R = (uint64_t)s.hlo * 66049u + __builtin_bit_cast(uint64_t, addend);
-        s.hhi = (uint32_t)(R >> 32);
-        s.hlo = (uint32_t)R;
-      }
+    for (int k = 0; k < 2; ++k) {
+      // acc*66049 + t = lo*66049 + {t, hi*66049}: a v_mul_lo_u32 for the
+      // high word feeds the 64-bit addend of ONE v_mad_u64_u32
+      const v2u32 addend = {t[k], s.hhi * 66049u};
+      const uint64_t R = (uint64_t)s.hlo * 66049u + __builtin_bit_cast(uint64_t, addend);
+      s.hhi = (uint32_t)(R >> 32);
+      s.hlo = (uint32_t)R;
     }
   }
-  if (ABL & ABL_NO_GEAR) return;
-  const int32_t m = (ABL & ABL_DWORD_SAMPLED) ? mx[3] : max(mx[3], (int32_t)g[3][3]);
-  if (ABL & ABL_NO_BRANCH) {
-    s.hhi ^= (uint32_t)m;
-    return;
-  }
-  if (ABL & ABL_NEVER) lo_thr = 0x7FFFFFFF;
+  const int32_t m = max(mx[3], (int32_t)g[3][3]);
   const uint64_t any = __ballot(m >= lo_thr);
   if (__builtin_expect(any != 0, 0)) {
-    if (ABL & ABL_NO_RECORD) {
-      wl.n += __popcll(any);
-      return;
-    }
     const uint32_t idx = wl.n + lane_prefix(any);
     if (m >= lo_thr && idx < ZC_WLIST) {
       wl.e[3 * idx] = ((rel >> 4) << 8) | last | (__lane_id() << 16);
@@ -570,30 +536,15 @@ __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, 
 // the next round's wait can leave them be.  A wave-tile whose list or pool
 // share overflowed is marked for the exact rescan (zc_anchor_rescan) and
 // stores no anchors.
-template <int ABL>
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
                                                   const uint64_t (&bk)[kDigests], const WaveList& wl,
                                                   uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
                                                   uint32_t& acc_pool, uint32_t& acc_over) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
-  if (ABL & ABL_TE_NO_STORE) {
-    uint32_t x = 0;
 #pragma unroll
-    for (int t = 0; t < kDigests; ++t) x ^= (uint32_t)bk[t] ^ (uint32_t)(bk[t] >> 32);
-    asm volatile("" ::"v"(x));
-    return 0;
-  }
-  if (ABL & ABL_TE_DIGEST_SAME) bo = (uint4*)(blk + (span0 % ZC_STILE) / ZC_SPAN);  // timing only: L2-hot
-#pragma unroll
-  for (int t = 0; t < kDigests / 2; ++t) {
-    const uint4 v = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
-                               (uint32_t)(bk[2 * t + 1] >> 32));
-    if (ABL & ABL_TE_DIGEST_NT)
-      __builtin_nontemporal_store(*(const v4u32*)&v, (v4u32*)(bo + t));
-    else
-      bo[t] = v;
-  }
-  if (ABL & ABL_TE_DIGEST_ONLY) return kDigests / 2;
+  for (int t = 0; t < kDigests / 2; ++t)
+    bo[t] = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
+                       (uint32_t)(bk[2 * t + 1] >> 32));
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)(wt - po.wt0) * po.wcap;
   uint32_t tot = 0, excl = 0, nst = 0;
@@ -657,10 +608,6 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
           i += 64;
         }
         if (__ballot(mask != 0) == 0) break;
-        if (ABL & ABL_TE_NO_ANCHOR_STORE) {
-          mask = 0;
-          continue;
-        }
         if (mask) {
           const uint32_t t = __builtin_ctz(mask), d = t >> 2, q = t & 3u;
           const uint32_t gdd = d == 0 ? gd[0] : d == 1 ? gd[1] : d == 2 ? gd[2] : gd[3];
@@ -700,7 +647,6 @@ struct ScanLds {
   uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
   uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 3];
 };
-template <int ABL>
 __device__ __forceinline__ void scan_body(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L) {
@@ -712,7 +658,6 @@ __device__ __forceinline__ void scan_body(
   const uint32_t grid = gridDim.x;
   uint8_t* myring = ring[wave];
   WaveList wl{wlist[wave], wdata[wave], 0};
-  if (ABL & ABL_PRIO) __builtin_amdgcn_s_setprio(3);  // ablation: issue ahead of co-resident kernels' waves
   const uint32_t ntk = ntiles > blockIdx.x ? (uint32_t)((ntiles - 1 - blockIdx.x) / grid + 1) : 0;
   const uint32_t nR = ntk * kRpt;
   // this lane's share of DMA instruction j: row j * (1024 / ZC_ROUND) + lane /
@@ -729,9 +674,8 @@ __device__ __forceinline__ void scan_body(
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kRpt, r = Rx - k * kRpt;
     const uint64_t tile = tile0 + blockIdx.x + (uint64_t)k * grid;
-    stage_round<((ABL & ABL_DMA_NT) ? 2 : 0) | ((ABL & ABL_DMA_SC1) ? 16 : 0)>(data, myring, wave, lane_off, tile,
-                                                                                  (int)r, Rx & 1);
-    if (!(ABL & ABL_NO_WARM) && r % kHalfRounds == 0) {
+    stage_round<kScanDmaAux>(data, myring, wave, lane_off, tile, (int)r, Rx & 1);
+    if (r % kHalfRounds == 0) {
       // span 0 of the stream has no bytes before it: it reads itself (unused)
       const uint64_t at = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN + (uint64_t)(r ^ hs) * ZC_ROUND;
       const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
@@ -739,12 +683,6 @@ __device__ __forceinline__ void scan_body(
       warm[1] = global_read16(src + 16);
     }
   };
-  if (ABL & (ABL_STAGGER_HALF | ABL_STAGGER_QUARTER)) {
-    // ablation: odd waves start later, so a SIMD's two waves reach their
-    // tile ends at different times
-    if (wave & 1)
-      for (int i = 0; i < ((ABL & ABL_STAGGER_HALF) ? 14 : 7); ++i) __builtin_amdgcn_s_sleep(127);
-  }
   if (nR > 0) issue(0);
   if (nR > 1) issue(1);
   ScanLane s{0, 0, 0};
@@ -765,7 +703,7 @@ __device__ __forceinline__ void scan_body(
     // plus the next half's warm-up loads before a half's first round, plus
     // the tile end's stores before round 0
     if (R + 1 >= nR) wait_vmcnt<0>();
-    else if ((r + 1) % kHalfRounds == 0) wait_vmcnt<(ABL & ABL_NO_WARM) ? kDmaRound : kDmaRound + 2>();
+    else if ((r + 1) % kHalfRounds == 0) wait_vmcnt<kDmaRound + 2>();
     else if (r == 0) wait_vmcnt_dyn(kDmaRound + tail_stores);
     else wait_vmcnt<kDmaRound>();
     const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND);
@@ -782,7 +720,7 @@ __device__ __forceinline__ void scan_body(
       // 32 bytes before only, so this equals the gear rolled on continuously)
       s.glo = 0;
       ties(warm);  // landed: the wait above covers them
-      if (!(ABL & ABL_NO_WARM) && span0 + pr * ZC_ROUND >= 64) {
+      if (span0 + pr * ZC_ROUND >= 64) {
         const uint32_t xs[8] = {warm[0][0], warm[0][1], warm[0][2], warm[0][3],
                                 warm[1][0], warm[1][1], warm[1][2], warm[1][3]};
 #pragma unroll
@@ -800,15 +738,15 @@ __device__ __forceinline__ void scan_body(
     // the first four pieces are hashed while the last four are still in flight
     wait_lgkmcnt<4>();
     ties(va);
-    const bool tile_end = r == kRounds - 1 && !(ABL & ABL_NO_TILE_END);
+    const bool tile_end = r == kRounds - 1;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) scan_piece<ABL>(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
+    for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
     wait_lgkmcnt<0>();  // the slot is free
     ties(vb);
     if (R + 2 < nR) issue(R + 2);
 #pragma unroll
     for (int p = 0; p < 4; ++p)
-      scan_piece<ABL>(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
+      scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const uint32_t q = pr / (ZC_SPAN / ZC_ROUND);  // per lane: the halves are rotated
@@ -816,20 +754,19 @@ __device__ __forceinline__ void scan_body(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (tile_end) tail_stores = scan_tile_end<ABL>(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
+    if (tile_end) tail_stores = scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
   }
-  if (!(ABL & ABL_NO_ATOMIC) && lane == 0) {
+  if (lane == 0) {
     if (acc_pool) atomicAdd(&counters[CNT_POOL], (unsigned long long)acc_pool);
     if (acc_over) atomicAdd(&counters[CNT_OVERFLOW], (unsigned long long)acc_over);
   }
 }
 
-template <int ABL>
 __global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
   __shared__ ScanLds lds;
-  scan_body<ABL>(data, n, tile0, ntiles, lo_thr, blk, po, counters, lds);
+  scan_body(data, n, tile0, ntiles, lo_thr, blk, po, counters, lds);
 }
 // the stream's last, partial tile: one 256-thread block per wave-tile, a
 // 1 KiB sub-span per thread (block digests and anchors)
@@ -2416,6 +2353,15 @@ __device__ __forceinline__ void sha1_block(uint32_t* st, const uint32_t* wbe) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // SHA-1 of [base, base + L) into out[20 i ..]
+// digest i (big-endian, 20 bytes) to out + 20 i as five dword stores (out is
+// 4-byte aligned: every digest buffer starts an allocation); the grid kernel's
+// out may be pinned host memory, where byte stores would each be a bus write
+__device__ __forceinline__ void put_digest(uint8_t* __restrict__ out, uint32_t i, const uint32_t* st) {
+  uint32_t* o = reinterpret_cast<uint32_t*>(out + (uint64_t)i * 20);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) o[k] = __builtin_bswap32(st[k]);
+}
+
 __device__ __forceinline__ void sha1_range(const uint8_t* __restrict__ data, uint64_t base, uint32_t L, uint32_t i,
                            uint8_t* __restrict__ out) {
   uint32_t st[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
@@ -2489,13 +2435,7 @@ __device__ __forceinline__ void sha1_range(const uint8_t* __restrict__ data, uin
     }
     sha1_block(st, w);
   }
-  for (int k = 0; k < 5; ++k) {
-    uint32_t v = st[k];
-    out[(uint64_t)i * 20 + 4 * k + 0] = v >> 24;
-    out[(uint64_t)i * 20 + 4 * k + 1] = v >> 16;
-    out[(uint64_t)i * 20 + 4 * k + 2] = v >> 8;
-    out[(uint64_t)i * 20 + 4 * k + 3] = v;
-  }
+  put_digest(out, i, st);
 }
 
 __global__ __launch_bounds__(64) void zc_sha1_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ a,
@@ -2566,13 +2506,7 @@ __device__ __forceinline__ void sha1_range16(const uint8_t* __restrict__ data, u
   w[14] = (uint32_t)(bits >> 32);
   w[15] = (uint32_t)bits;
   sha1_block(st, w);
-  for (int k = 0; k < 5; ++k) {
-    const uint32_t v = st[k];
-    out[(uint64_t)i * 20 + 4 * k + 0] = v >> 24;
-    out[(uint64_t)i * 20 + 4 * k + 1] = v >> 16;
-    out[(uint64_t)i * 20 + 4 * k + 2] = v >> 8;
-    out[(uint64_t)i * 20 + 4 * k + 3] = v;
-  }
+  put_digest(out, i, st);
 }
 
 // the whole grid chunks i < nr, each [i W, (i + 1) W), W = 0 mod 16
@@ -2629,7 +2563,7 @@ hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, ui
                              uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
   if (!ntiles) return hipSuccess;
   const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
-  hipLaunchKernelGGL(zc_scan_kernel<kScanProduct>, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles,
+  hipLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles,
                      anchor_lo, blk, po, counters);
   return hipGetLastError();
 }
