@@ -300,11 +300,14 @@ class SpinTeam {
 // records of grid chunks k0 .. k0 + n - 1 of an epoch at r0 (offset r0 + k W,
 // size W, one kind, rolling hash key[k] or 0), in parallel when many: two
 // 40-byte records are five 16-byte words, streamed past the caches (no
-// read-for-ownership of the lines they overwrite)
+// read-for-ownership of the lines they overwrite) -- unless the records' SHA-1
+// prefixes are written into them later (ZC_FLAG_SHA1): then the lines stay in
+// the writing threads' caches, where the same team's fill finds them (the
+// parts are the same record ranges), instead of being fetched back from DRAM
 constexpr uint64_t kParallelRecordsMin = 32768;
 
 void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uint32_t W, uint32_t kind,
-                       const uint64_t* key) {
+                       const uint64_t* key, bool stream) {
   auto fill = [&](size_t a, size_t b) {
     auto put = [&](size_t j) {
       zc_record& r = out[j];
@@ -321,14 +324,16 @@ void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uin
       const uint64_t o0 = r0 + (k0 + j) * W, o1 = o0 + W;
       const uint64_t h0 = key ? key[k0 + j] : 0, h1 = key ? key[k0 + j + 1] : 0;
       __m128i* d = (__m128i*)(out + j);
-      _mm_stream_si128(d + 0, _mm_set_epi64x((long long)sk, (long long)o0));
-      _mm_stream_si128(d + 1, _mm_set_epi64x(0, (long long)h0));
-      _mm_stream_si128(d + 2, _mm_set_epi64x((long long)o1, 0));
-      _mm_stream_si128(d + 3, _mm_set_epi64x((long long)h1, (long long)sk));
-      _mm_stream_si128(d + 4, _mm_setzero_si128());
+      const __m128i v[5] = {_mm_set_epi64x((long long)sk, (long long)o0), _mm_set_epi64x(0, (long long)h0),
+                            _mm_set_epi64x((long long)o1, 0), _mm_set_epi64x((long long)h1, (long long)sk),
+                            _mm_setzero_si128()};
+      if (stream)
+        for (int u = 0; u < 5; ++u) _mm_stream_si128(d + u, v[u]);
+      else
+        for (int u = 0; u < 5; ++u) _mm_store_si128(d + u, v[u]);
     }
     for (; j < b; ++j) put(j);
-    _mm_sfence();
+    if (stream) _mm_sfence();
   };
   if (n >= kParallelRecordsMin) SpinTeam::get().run(n, fill);  // (armed by the epoch before its wait)
   else fill(0, n);
@@ -1970,6 +1975,10 @@ class Resolver {
 
   // ---------------------------------------------------------------- walk
 
+  // grid records are streamed past the caches unless their SHA-1 prefixes
+  // are filled in after the grid SHA-1 lands (fill_grid_records)
+  bool stream_recs() const { return !pre_sha_n_; }
+
   void push(uint64_t off, uint32_t size, uint32_t kind, uint64_t rolling) {
     zc_record r;
     memset(&r, 0, sizeof r);
@@ -2005,7 +2014,7 @@ class Resolver {
     const uint8_t* dead = indexable_ ? dead_.data() + nconf_ : nullptr;
     if (ndead_ == 0 && r_e_ + ks_ * W_ >= s_ && kmax - ks_ >= kParallelRecords) {
       // every chunk of the run is saved: record o + j is grid chunk ks_ + j
-      fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr);
+      fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr, stream_recs());
       s_ = r_e_ + kmax * W_;
       ks_ = kmax;
       return;
@@ -2067,7 +2076,7 @@ class Resolver {
     if (!nchain) return;
     const size_t o = c_.recs.size();
     c_.recs.resize(o + nchain);
-    fill_grid_records(c_.recs.data() + o, nchain, r_e_, j + 1, W_, ZC_CHUNK_DUP, c_.h_key.p);
+    fill_grid_records(c_.recs.data() + o, nchain, r_e_, j + 1, W_, ZC_CHUNK_DUP, c_.h_key.p, stream_recs());
     r_ = r_e_ + (uint64_t)jn * W_;
     s_ = r_;
     if (jn > ks_) ks_ = jn;
