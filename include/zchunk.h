@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ZCHUNK_ABI_VERSION 3
+#define ZCHUNK_ABI_VERSION 4
 
 enum zc_status {
   ZC_OK = 0,
@@ -109,6 +109,8 @@ typedef struct {
   double sha_fill_ms;    /* after it: SHA-1 prefixes into the records, the new chunks' index entries completed */
   double hist_ms;        /* before it: the stream's new chunks joining the context's index (keys, anchors) */
   uint64_t respeculations; /* streams redone because a speculative key + SHA-1 class join proved wrong */
+  /* ABI 4: */
+  uint64_t chk_rebuilds;   /* the one-level static screen's check table rebuilt larger for an epoch's own keys */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;

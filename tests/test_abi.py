@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version_and_argument_errors(lib):
     import ctypes
-    assert lib.zc_abi_version() == 3
+    assert lib.zc_abi_version() == 4
     ctx = ctypes.c_void_p()
     assert lib.zc_create(None, 65536, 0, 0) == _lib.ZC_ERR_ARG
     assert lib.zc_create(ctypes.byref(ctx), 0, 0, 0) == _lib.ZC_ERR_ARG  # chunk.max_size 0

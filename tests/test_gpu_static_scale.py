@@ -108,3 +108,41 @@ def test_bloom_screen_odd_w_vs_oracle(torch_cuda, W, nrand):
     with BackupCreator(W, seeds=seeds, sha1=True) as bc:
         bc.chunk_device(t.data_ptr(), data.size)
         _same(bc.records(), want)
+
+
+def _headed_blocks(nblk, W, seed):
+    """nblk W-byte blocks, each 32 seeded random bytes then zeros: all distinct,
+    none with an anchor (a chunk's first anchor sits at offset >= 63, where
+    the 32-byte gear window sees only zeros)."""
+    rng = np.random.default_rng(seed)
+    b = np.zeros((nblk, W), dtype=np.uint8)
+    b[:, :32] = rng.integers(0, 256, (nblk, 32), dtype=np.uint8)
+    return b.reshape(-1)
+
+
+def test_check_table_overflow_rebuilds_vs_oracle(torch_cuda, monkeypatch):
+    """An epoch whose own anchorless keys do not fit the one-level screen's check
+    table (the by-value set's table plus room for 65,536 epoch keys): the table
+    is rebuilt with room for them and the one-level screen kept.  Forced here:
+    ZC_TEST_CHK_BITS starts the table's size search so small that it ends
+    barely holding the 400 K seeded keys, and the 72 MB stream is ~590 K
+    distinct anchorless chunks, every one of whose keys joins the epoch's copy
+    of the table; 400 seeded ids are blocks the stream repeats (matches)."""
+    from zbackup_amd import BackupCreator
+    W = 128
+    old = _headed_blocks(2000, W, 7)
+    real = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in oracle.chunk(old, W) if k == "N" and s == W][:400]
+    rng = np.random.default_rng(48)
+    keys = rng.integers(1, 2**63, 400000, dtype=np.int64)
+    shas = rng.integers(0, 256, (400000, 16), dtype=np.uint8)
+    seeds = real + [(shas[i].tobytes(), int(keys[i]), W) for i in range(400000)]
+    data = np.concatenate([_headed_blocks(300000, W, 8), oracle.gen("R5:77"), old[:51200],
+                           _headed_blocks(290000, W, 9)])
+    want = oracle.chunk_array(data, W, seeds=seeds)
+    assert (want["kind"] == 1).sum() >= len(real)
+    monkeypatch.setenv("ZC_TEST_CHK_BITS", "12")
+    t = torch_cuda.from_numpy(data).to("cuda")
+    with BackupCreator(W, seeds=seeds, sha1=True) as bc:
+        bc.chunk_device(t.data_ptr(), data.size)
+        _same(bc.records(), want)
+        assert bc.stats()["chk_rebuilds"] >= 1

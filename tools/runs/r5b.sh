@@ -4,7 +4,7 @@ set -e
 export TMPDIR=/tmp
 O=gpurun_out/r5b
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_chain.py tests/test_gpu_window.py > $O/pytest.txt 2>&1
+timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_chain.py tests/test_gpu_window.py tests/test_gpu_static_scale.py > $O/pytest.txt 2>&1
 timeout -k 10 200 python tools/sha_steps.py 4 > $O/sha_steps.txt 2>&1
 ZC_DEBUG_FILL=1 timeout -k 10 200 python bench.py --sha1 --steps 5 --no-cpu-baseline --no-extras > $O/fill.txt 2>&1
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras > $O/bench_headline.txt 2>&1

@@ -43,7 +43,7 @@ class ZcStats(ctypes.Structure):
                 ("window_bytes", ctypes.c_uint64), ("hbm_bytes", ctypes.c_uint64),
                 ("segments", ctypes.c_uint64), ("hist_entries", ctypes.c_uint64),
                 ("sha_wait_ms", ctypes.c_double), ("sha_fill_ms", ctypes.c_double), ("hist_ms", ctypes.c_double),
-                ("respeculations", ctypes.c_uint64)]
+                ("respeculations", ctypes.c_uint64), ("chk_rebuilds", ctypes.c_uint64)]
 
 
 class ZcError(RuntimeError):

@@ -341,6 +341,10 @@ void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uin
 
 class Resolver;
 
+// the one-level screen's check table holds the by-value set plus this many of
+// an epoch's own anchorless keys (grown when an epoch brings more)
+constexpr uint64_t kChkRoomDefault = 65536;
+
 }  // namespace
 
 struct zc_ctx {
@@ -388,6 +392,7 @@ struct zc_ctx {
   DevBuf<uint16_t> chk_s, chk_w;
   DevBuf<unsigned int> chk_ovf;
   uint32_t chk_bits = 0;
+  uint64_t chk_room = kChkRoomDefault;  // epoch keys the check table leaves room for
   bool bloom_one = false;
   DevBuf<uint64_t> kset;              // 64-bit keys, open addressing (empty = 0)
   uint32_t kset_bits = 0;
@@ -528,9 +533,12 @@ void statics_screen(zc_ctx& c) {
   c.bloom_s.ensure(bloom.size());
   c.bloom_one = keys.size() + 64 >= kBloomOneLevelMin;
   if (c.bloom_one) {
-    // room for the epochs' own keys too (launch_chk_add); a chain that would
-    // reach the last bucket makes the table twice as large
-    for (c.chk_bits = chk_bits_for(keys.size() + 65536);; ++c.chk_bits) {
+    // room for the epochs' own keys too (launch_chk_add: chk_room of them, more
+    // after an epoch overflowed it); a chain that would reach the last bucket
+    // makes the table twice as large.  (ZC_TEST_CHK_BITS: tests start the
+    // search from a table too small for any epoch keys, to force that overflow.)
+    const char* tb = c.chk_room == kChkRoomDefault ? getenv("ZC_TEST_CHK_BITS") : nullptr;
+    for (c.chk_bits = tb ? (uint32_t)atoi(tb) : chk_bits_for(keys.size() + c.chk_room);; ++c.chk_bits) {
       const uint64_t nb = (1ull << c.chk_bits) + kChkPad;
       std::vector<uint16_t> chk(nb * 4, 0);
       bool fits = true;
@@ -1569,15 +1577,25 @@ class Resolver {
         HCK(launch_bloom_add(c_.bloom_w.p, c_.bloom_bits, c_.flist.p, (uint32_t)fk.size(), c_.stream));
         bloom_p_ = c_.bloom_w.p;
         if (c_.bloom_one) {  // and a copy of the check table
-          const size_t nw = ((1ull << c_.chk_bits) + kChkPad) * 4;
-          c_.chk_w.ensure(nw);
-          HCK(hipMemcpyAsync(c_.chk_w.p, c_.chk_s.p, sizeof(uint16_t) * nw, hipMemcpyDeviceToDevice, c_.stream));
-          HCK(hipMemsetAsync(c_.chk_ovf.p, 0, sizeof(unsigned int), c_.stream));
-          HCK(launch_chk_add(c_.chk_w.p, c_.chk_bits, c_.flist.p, (uint32_t)fk.size(), c_.chk_ovf.p, c_.stream));
-          unsigned int ovf = 0;
-          d2h(c_, &ovf, c_.chk_ovf.p, 1);
-          sync(c_);
-          chk_p_ = ovf ? nullptr : c_.chk_w.p;  // full: the two-level screen
+          for (;;) {
+            const size_t nw = ((1ull << c_.chk_bits) + kChkPad) * 4;
+            c_.chk_w.ensure(nw);
+            HCK(hipMemcpyAsync(c_.chk_w.p, c_.chk_s.p, sizeof(uint16_t) * nw, hipMemcpyDeviceToDevice, c_.stream));
+            HCK(hipMemsetAsync(c_.chk_ovf.p, 0, sizeof(unsigned int), c_.stream));
+            HCK(launch_chk_add(c_.chk_w.p, c_.chk_bits, c_.flist.p, (uint32_t)fk.size(), c_.chk_ovf.p, c_.stream));
+            unsigned int ovf = 0;
+            d2h(c_, &ovf, c_.chk_ovf.p, 1);
+            sync(c_);
+            if (!ovf) break;
+            // the epoch's keys did not fit: rebuild the set's table with room
+            // for them (the one-level screen stays: the two-level one's filter
+            // is sized for other key counts) and add them again
+            c_.chk_room = std::max<uint64_t>(2 * c_.chk_room, 2 * fk.size());
+            c_.sc_ver = 0;
+            statics_screen(c_);
+            ++c_.stats.chk_rebuilds;
+          }
+          chk_p_ = c_.chk_w.p;
         }
       }
     } else if (nf > 16) {
