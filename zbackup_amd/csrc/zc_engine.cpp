@@ -226,7 +226,7 @@ class SpinTeam {
   // f(begin, end) over [0, n) in kParts parts; the helpers that are not
   // spinning (not armed, or past the deadline) are not waited for: their
   // parts run on this thread
-  void run(size_t n, const std::function<void(size_t, size_t)>& f) {
+  int run(size_t n, const std::function<void(size_t, size_t)>& f) {
     std::lock_guard<std::mutex> one(run_);
     job_ = &f;
     n_ = n;
@@ -244,6 +244,7 @@ class SpinTeam {
       }
     while (done_.load(std::memory_order_acquire) + mine < kParts) _mm_pause();
     job_ = nullptr;
+    return mine;  // parts done here (kParts: no helper was spinning)
   }
 
  private:
@@ -660,6 +661,7 @@ class Resolver {
     hist0_ = c_.nhist;
     statics0_ = c_.statics.size();
     r_ = s_ = x_resume_ = hspan_ = 0;
+    gruns_.clear();
     scan_setup();
   }
   // bytes [0, n) of the stream are (being) copied to the device, in order on
@@ -1995,7 +1997,19 @@ class Resolver {
 
   // grid records are streamed past the caches unless their SHA-1 prefixes
   // are filled in after the grid SHA-1 lands (fill_grid_records)
-  bool stream_recs() const { return !pre_sha_n_; }
+  bool stream_recs() const {
+    static const bool cached = getenv("ZC_REC_CACHED") != nullptr;  // TEMP (round-5 A/B)
+    return !(pre_sha_n_ && cached);
+  }
+  // the runs of records fill_grid_records wrote since the last finalize:
+  // records rec0 .. rec0 + n - 1 are [off0 + j W, off0 + (j + 1) W), one kind;
+  // finalize_records classifies them without reading them back
+  struct GridRun {
+    size_t rec0;
+    uint64_t n, off0;
+    uint32_t kind;
+  };
+  std::vector<GridRun> gruns_;
 
   void push(uint64_t off, uint32_t size, uint32_t kind, uint64_t rolling) {
     zc_record r;
@@ -2033,6 +2047,7 @@ class Resolver {
     if (ndead_ == 0 && r_e_ + ks_ * W_ >= s_ && kmax - ks_ >= kParallelRecords) {
       // every chunk of the run is saved: record o + j is grid chunk ks_ + j
       fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr, stream_recs());
+      gruns_.push_back({o, kmax - ks_, r_e_ + ks_ * W_, kind});
       s_ = r_e_ + kmax * W_;
       ks_ = kmax;
       return;
@@ -2095,6 +2110,7 @@ class Resolver {
     const size_t o = c_.recs.size();
     c_.recs.resize(o + nchain);
     fill_grid_records(c_.recs.data() + o, nchain, r_e_, j + 1, W_, ZC_CHUNK_DUP, c_.h_key.p, stream_recs());
+    gruns_.push_back({o, nchain, r_e_ + (j + 1) * W_, (uint32_t)ZC_CHUNK_DUP});
     r_ = r_e_ + (uint64_t)jn * W_;
     s_ = r_;
     if (jn > ks_) ks_ = jn;
@@ -2360,11 +2376,17 @@ class Resolver {
     need_digest_.clear();
     const size_t r0 = c_.nrec_done, r1 = c_.recs.size();
     const bool sha1 = c_.flags & ZC_FLAG_SHA1;
+    struct ClearRuns {
+      std::vector<GridRun>& v;
+      ~ClearRuns() { v.clear(); }
+    } clear_runs{gruns_};
     if (!sha1) {
       c_.nrec_done = r1;
       if (stream_end) stream_end_index(nullptr);
       return;
     }
+    // the fill team, awake by the time the digests land
+    if (r1 - r0 >= kParallelRecordsMin) SpinTeam::get().arm();
     // records that are a whole grid chunk take their SHA-1 from the side
     // stream's pass; the others are hashed now
     const bool pow2 = (W_ & (W_ - 1)) == 0;
@@ -2384,7 +2406,36 @@ class Resolver {
     const size_t f0 = fresh_.size();
     gq.reserve(r1 - r0);
     gslot.reserve(r1 - r0);
+    frec.reserve(r1 - r0);
+    size_t gr = 0;
+    while (gr < gruns_.size() && gruns_[gr].rec0 < r0) ++gr;
     for (size_t i = r0; i < r1; ++i) {
+      if (gr < gruns_.size() && gruns_[gr].rec0 == i) {
+        // a run of grid-aligned records written by fill_grid_records: its
+        // chunks, fresh entries and index slots follow from the run alone
+        const GridRun& g = gruns_[gr++];
+        const bool on_grid = g.off0 % W_ == 0 && g.kind != ZC_BYTES;
+        const uint64_t q0 = g.off0 / W_;
+        for (uint64_t j = 0; j < g.n; ++j) {
+          uint32_t slot = kNoSlot;
+          if (g.kind == ZC_CHUNK_NEW) {
+            slot = (uint32_t)frec.size();
+            fresh_.push_back(g.off0 + j * W_);
+            frec.push_back((uint32_t)(i + j - r0));
+          }
+          if (on_grid && q0 + j < pre_sha_n_ && g.off0 + (j + 1) * W_ <= n_) {
+            gq.push_back((uint64_t)(i + j - r0) << 32 | (q0 + j));
+            gslot.push_back(slot);
+          } else if (g.kind != ZC_BYTES) {
+            if (slot != kNoSlot) fsh.push_back((uint32_t)idx.size());
+            sa.push_back(g.off0 + j * W_);
+            sl.push_back(W_);
+            idx.push_back(i + j);
+          }
+        }
+        i += g.n - 1;
+        continue;
+      }
       const zc_record& r = c_.recs[i];
       if (r.kind == ZC_BYTES) continue;
       uint32_t slot = kNoSlot;
@@ -2404,6 +2455,7 @@ class Resolver {
       sl.push_back(r.size);
       idx.push_back(i);
     }
+    const double t_class = ms_since(t0);
     std::vector<uint8_t> sh = sha1s(sa, sl);
     HistPending hp;
     auto th = Clock::now();
@@ -2423,7 +2475,6 @@ class Resolver {
       fs = fresh_sha_.data() + 16 * f0;
     }
     const bool team = gq.size() >= kParallelRecordsMin;
-    if (team) SpinTeam::get().arm();  // awake by the time the digests land
     auto tw = Clock::now();
     const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;  // waits for the side stream
     c_.stats.sha_wait_ms += ms_since(tw);
@@ -2453,7 +2504,8 @@ class Resolver {
       }
       _mm_sfence();
     };
-    if (team) SpinTeam::get().run(gq.size(), fill);
+    int mine = -1;
+    if (team) mine = SpinTeam::get().run(gq.size(), fill);
     else fill(0, gq.size());
     for (size_t j = 0; j < idx.size(); ++j) memcpy(c_.recs[idx[j]].sha1, &sh[j * 20], 16);
     for (uint32_t t : fsh) {  // new chunks hashed here: their slot is their place among frec
@@ -2466,8 +2518,9 @@ class Resolver {
     if (stream_end) stream_end_index(&hp, in_place);
     c_.stats.sha_fill_ms += ms_since(tf);
     if (getenv("ZC_DEBUG_FILL"))  // TEMP (round-5 measurement)
-      fprintf(stderr, "fill %.3f end %.3f (gq %zu frec %zu)\n", t_fill, ms_since(tf) - t_fill, gq.size(),
-              frec.size());
+      fprintf(stderr, "classify %.3f hist %.3f wait %.3f fill %.3f (main did %d parts) end %.3f (gq %zu frec %zu)\n",
+              t_class, ms_since(th) - ms_since(tw), ms_since(tw) - ms_since(tf), t_fill, mine, ms_since(tf) - t_fill,
+              gq.size(), frec.size());
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
