@@ -900,14 +900,28 @@ class Resolver {
   // sha16: the entries' SHA-1 prefixes, 16 bytes each; entries without an
   // anchor also join the by-value set of the exact screen
   // (sha16 null: already in place in c_.hsha)
-  void hist_add_sha(const HistPending& hp, const uint8_t* sha16) {
+  // (ancless: the entries without an anchor when already known, see
+  // ancless_of; else found here)
+  void hist_add_sha(const HistPending& hp, const uint8_t* sha16, const std::vector<uint32_t>* ancless = nullptr) {
     if (!hp.k) return;
-    sync(c_);  // hp.anc has landed
+    std::vector<uint32_t> own;
+    if (!ancless) {
+      own = ancless_of(hp);
+      ancless = &own;
+    }
     c_.hsha.resize(16 * ((size_t)hp.e0 + hp.k));
     uint8_t* hs = c_.hsha.data() + 16 * (size_t)hp.e0;
     if (sha16) memcpy(hs, sha16, 16 * (size_t)hp.k);
+    for (uint32_t i : *ancless) add_static_once(c_, c_.hkey[hp.e0 + i], hs + 16 * (size_t)i, 0);
+  }
+  // the pending entries without an anchor (they join the by-value set too)
+  std::vector<uint32_t> ancless_of(const HistPending& hp) {
+    std::vector<uint32_t> v;
+    if (!hp.k) return v;
+    sync(c_);  // hp.anc has landed
     for (uint32_t i = 0; i < hp.k; ++i)
-      if (hp.anc[i] == ZC_NO_ANCHOR) add_static_once(c_, c_.hkey[hp.e0 + i], hs + 16 * (size_t)i, 0);
+      if (hp.anc[i] == ZC_NO_ANCHOR) v.push_back(i);
+    return v;
   }
 
  private:
@@ -2374,6 +2388,7 @@ class Resolver {
     std::vector<uint64_t> h = range_digests(a, b);
     for (size_t j = 0; j < rest.size(); ++j) c_.recs[need_digest_[rest[j]].rec].rolling = h[j];
     need_digest_.clear();
+    const double t_dig = ms_since(t0);
     const size_t r0 = c_.nrec_done, r1 = c_.recs.size();
     const bool sha1 = c_.flags & ZC_FLAG_SHA1;
     struct ClearRuns {
@@ -2407,6 +2422,7 @@ class Resolver {
     gq.reserve(r1 - r0);
     gslot.reserve(r1 - r0);
     frec.reserve(r1 - r0);
+    fresh_.reserve(fresh_.size() + (r1 - r0));
     size_t gr = 0;
     while (gr < gruns_.size() && gruns_[gr].rec0 < r0) ++gr;
     for (size_t i = r0; i < r1; ++i) {
@@ -2459,7 +2475,11 @@ class Resolver {
     std::vector<uint8_t> sh = sha1s(sa, sl);
     HistPending hp;
     auto th = Clock::now();
-    if (stream_end) hp = hist_add_meta(fresh_);
+    std::vector<uint32_t> hp_ancless;
+    if (stream_end) {
+      hp = hist_add_meta(fresh_);
+      hp_ancless = ancless_of(hp);  // (its work ran beside the SHA-1 kernel: done by now)
+    }
     c_.stats.hist_ms += ms_since(th);
     // the new W-byte chunks' SHA-1 prefixes, in record order as fresh_: at
     // the stream's end straight into the historic index (their entries
@@ -2478,10 +2498,23 @@ class Resolver {
     auto tw = Clock::now();
     const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;  // waits for the side stream
     c_.stats.sha_wait_ms += ms_since(tw);
-    for (const auto& pq : spec_pairs_)  // the speculated joins (epoch)
-      if (memcmp(gsha + 20 * pq.first, gsha + 20 * pq.second, 16) != 0) throw Respeculate{};
-    spec_pairs_.clear();
     auto tf = Clock::now();
+    const size_t npairs = spec_pairs_.size();
+    {
+      // the speculated joins (epoch): every pair's prefixes must agree
+      std::atomic<bool> refuted{false};
+      auto check = [&](size_t a, size_t b) {
+        for (size_t j = a; j < b; ++j)
+          if (memcmp(gsha + 20 * spec_pairs_[j].first, gsha + 20 * spec_pairs_[j].second, 16) != 0) {
+            refuted.store(true, std::memory_order_relaxed);
+            return;
+          }
+      };
+      if (spec_pairs_.size() >= kParallelRecordsMin) SpinTeam::get().run(spec_pairs_.size(), check);
+      else check(0, spec_pairs_.size());
+      if (refuted.load()) throw Respeculate{};
+      spec_pairs_.clear();
+    }
     zc_record* const rb = c_.recs.data() + r0;
     // one pass: each grid-chunk record's prefix from the side stream's
     // digests, into the record and, for a new chunk, its index slot; the
@@ -2515,12 +2548,14 @@ class Resolver {
     }
     const double t_fill = ms_since(tf);
     c_.nrec_done = r1;
-    if (stream_end) stream_end_index(&hp, in_place);
+    if (stream_end) stream_end_index(&hp, in_place, &hp_ancless);
     c_.stats.sha_fill_ms += ms_since(tf);
     if (getenv("ZC_DEBUG_FILL"))  // TEMP (round-5 measurement)
-      fprintf(stderr, "classify %.3f hist %.3f wait %.3f fill %.3f (main did %d parts) end %.3f (gq %zu frec %zu)\n",
-              t_class, ms_since(th) - ms_since(tw), ms_since(tw) - ms_since(tf), t_fill, mine, ms_since(tf) - t_fill,
-              gq.size(), frec.size());
+      fprintf(stderr,
+              "digests %.3f classify %.3f hist %.3f wait %.3f checks+fill %.3f (main did %d parts) end %.3f (gq %zu "
+              "frec %zu pairs %zu)\n",
+              t_dig, t_class - t_dig, ms_since(th) - ms_since(tw), ms_since(tw) - ms_since(tf), t_fill, mine,
+              ms_since(tf) - t_fill, gq.size(), frec.size(), npairs);
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
@@ -2529,9 +2564,10 @@ class Resolver {
   // matches a committed one's index (chunk_index.cc:26-79).  Without it the
   // index is left as the stream found it (entries evicted from the window
   // during the stream are dropped again).
-  void stream_end_index(const HistPending* hp, bool sha_in_place = false) {
+  void stream_end_index(const HistPending* hp, bool sha_in_place = false,
+                        const std::vector<uint32_t>* ancless = nullptr) {
     if (c_.flags & ZC_FLAG_SHA1) {
-      hist_add_sha(*hp, sha_in_place ? nullptr : fresh_sha_.data());
+      hist_add_sha(*hp, sha_in_place ? nullptr : fresh_sha_.data(), ancless);
     } else {
       index_truncate(c_, hist0_, statics0_);
     }

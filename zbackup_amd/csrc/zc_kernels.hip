@@ -2290,28 +2290,33 @@ constexpr uint64_t kKey64FilterMax = 64;  // longer runs are left to the walk
 // thread per screen run: a short run keeps only [first, last] of the
 // positions whose 64-bit window key (257^W + the window's accumulator) is
 // in the sets; none: the run becomes empty
-__global__ void zc_key64_filter_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk, uint32_t W,
-                                       uint64_t pw, Run* __restrict__ runs, uint64_t nruns,
-                                       const uint64_t* __restrict__ set, uint32_t sbits, int zero_key,
-                                       const uint64_t* __restrict__ list, uint32_t nl) {
+__global__ void __launch_bounds__(64) zc_key64_filter_kernel(const uint8_t* __restrict__ data,
+                                                             const uint64_t* __restrict__ blk, uint32_t W, uint64_t pw,
+                                                             Run* __restrict__ runs, uint64_t nruns,
+                                                             const uint64_t* __restrict__ set, uint32_t sbits,
+                                                             int zero_key, const uint64_t* __restrict__ list,
+                                                             uint32_t nl) {
   ZC_URGENT();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // one wave per run, one position per lane (a run is at most 64 positions):
+  // each lane's exact key is an independent fold, so the wave computes the
+  // run's keys side by side instead of one lane walking them in turn
+  static_assert(kKey64FilterMax <= 64, "a lane per position");
+  const uint64_t i = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
   if (i >= nruns) return;
   const Run r = runs[i];
   if (r.end - r.start > kKey64FilterMax) return;
-  uint64_t first = ~0ull, last = 0;
-  for (uint64_t p = r.start; p < r.end; ++p) {
-    const uint64_t k = pw + rk_acc(data, blk, p + 1 - W, p + 1);
-    if (key64_in(k, set, sbits, zero_key, list, nl)) {
-      if (first == ~0ull) first = p;
-      last = p;
+  const uint64_t p = r.start + lane;
+  bool hit = false;
+  if (p < r.end) hit = key64_in(pw + rk_acc(data, blk, p + 1 - W, p + 1), set, sbits, zero_key, list, nl);
+  const uint64_t m = __ballot(hit);
+  if (lane == 0) {
+    if (!m) {
+      runs[i].end = r.start;
+    } else {
+      runs[i].start = r.start + (uint64_t)__builtin_ctzll(m);
+      runs[i].end = r.start + 64 - (uint64_t)__builtin_clzll(m);
     }
-  }
-  if (first == ~0ull) {
-    runs[i].end = r.start;
-  } else {
-    runs[i].start = first;
-    runs[i].end = last + 1;
   }
 }
 
@@ -2849,8 +2854,9 @@ hipError_t launch_key64_filter(const uint8_t* data, const uint64_t* blk, uint32_
                                uint64_t nruns, const uint64_t* set, uint32_t sbits, int zero_key,
                                const uint64_t* list, uint32_t nl, hipStream_t s) {
   if (!nruns) return hipSuccess;
-  hipLaunchKernelGGL(zc_key64_filter_kernel, dim3(blocks_for(nruns, 64)), dim3(64), 0, s, data, blk, W, pw, runs,
-                     nruns, set, sbits, zero_key, list, nl);
+  if (nruns > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(zc_key64_filter_kernel, dim3((unsigned)nruns), dim3(64), 0, s, data, blk, W, pw, runs, nruns, set,
+                     sbits, zero_key, list, nl);
   return hipGetLastError();
 }
 
