@@ -301,14 +301,13 @@ class SpinTeam {
 // records of grid chunks k0 .. k0 + n - 1 of an epoch at r0 (offset r0 + k W,
 // size W, one kind, rolling hash key[k] or 0), in parallel when many: two
 // 40-byte records are five 16-byte words, streamed past the caches (no
-// read-for-ownership of the lines they overwrite) -- unless the records' SHA-1
-// prefixes are written into them later (ZC_FLAG_SHA1): then the lines stay in
-// the writing threads' caches, where the same team's fill finds them (the
-// parts are the same record ranges), instead of being fetched back from DRAM
+// read-for-ownership of the lines they overwrite).  (With ZC_FLAG_SHA1 the
+// records' prefixes are written into them after the grid SHA-1 lands; writing
+// the records through the caches for that measured the same, round 5.)
 constexpr uint64_t kParallelRecordsMin = 32768;
 
 void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uint32_t W, uint32_t kind,
-                       const uint64_t* key, bool stream) {
+                       const uint64_t* key) {
   auto fill = [&](size_t a, size_t b) {
     auto put = [&](size_t j) {
       zc_record& r = out[j];
@@ -325,16 +324,14 @@ void fill_grid_records(zc_record* out, uint64_t n, uint64_t r0, uint64_t k0, uin
       const uint64_t o0 = r0 + (k0 + j) * W, o1 = o0 + W;
       const uint64_t h0 = key ? key[k0 + j] : 0, h1 = key ? key[k0 + j + 1] : 0;
       __m128i* d = (__m128i*)(out + j);
-      const __m128i v[5] = {_mm_set_epi64x((long long)sk, (long long)o0), _mm_set_epi64x(0, (long long)h0),
-                            _mm_set_epi64x((long long)o1, 0), _mm_set_epi64x((long long)h1, (long long)sk),
-                            _mm_setzero_si128()};
-      if (stream)
-        for (int u = 0; u < 5; ++u) _mm_stream_si128(d + u, v[u]);
-      else
-        for (int u = 0; u < 5; ++u) _mm_store_si128(d + u, v[u]);
+      _mm_stream_si128(d + 0, _mm_set_epi64x((long long)sk, (long long)o0));
+      _mm_stream_si128(d + 1, _mm_set_epi64x(0, (long long)h0));
+      _mm_stream_si128(d + 2, _mm_set_epi64x((long long)o1, 0));
+      _mm_stream_si128(d + 3, _mm_set_epi64x((long long)h1, (long long)sk));
+      _mm_stream_si128(d + 4, _mm_setzero_si128());
     }
     for (; j < b; ++j) put(j);
-    if (stream) _mm_sfence();
+    _mm_sfence();
   };
   if (n >= kParallelRecordsMin) SpinTeam::get().run(n, fill);  // (armed by the epoch before its wait)
   else fill(0, n);
@@ -401,7 +398,7 @@ struct zc_ctx {
   DevBuf<uint64_t> flist;  // the epoch's anchorless keys, sorted (64-bit)
   // historic index: this context's W-byte chunks whose bytes are gone from HBM
   // (earlier streams, or evicted from the window), each with its first anchor
-  std::vector<uint64_t> hkey;
+  std::vector<uint64_t, DefaultInit<uint64_t>> hkey;  // (resize leaves new entries to be written)
   std::vector<uint8_t, DefaultInit<uint8_t>> hsha;  // 16 bytes per entry (resize leaves them to be written)
   uint32_t nhist = 0;
   DevBuf<uint32_t> hanc, hg;
@@ -414,6 +411,9 @@ struct zc_ctx {
   // being cut.  The taken prefix is dropped once it is most of the vector, so
   // draining a long stream in small batches stays linear.
   std::vector<zc_record, DefaultInit<zc_record>> recs;  // resize leaves new records to be written
+  // the resolver's per-stream lists, kept here for their capacity (Resolver)
+  std::vector<uint64_t> fin_gq, fin_fresh;
+  std::vector<uint32_t> fin_gslot, fin_frec;
   size_t nrec_done = 0;
   size_t rec_head = 0;
   // every entry point holds this: calls on one context from several threads
@@ -662,6 +662,7 @@ class Resolver {
     statics0_ = c_.statics.size();
     r_ = s_ = x_resume_ = hspan_ = 0;
     gruns_.clear();
+    fresh_.clear();
     scan_setup();
   }
   // bytes [0, n) of the stream are (being) copied to the device, in order on
@@ -1191,7 +1192,6 @@ class Resolver {
     f_min_vis_ = kInf;
     uint64_t ncand = 0, nancless = 0;
     const HistTab ht = hist_tab();
-    if (sha_behind_scan()) sha_launch();  // beside the batch, whose kernels take issue priority
     if (nref_ || ht.tab) {
       auto tm = Clock::now();
       EpochIndex ix{};
@@ -2009,12 +2009,6 @@ class Resolver {
 
   // ---------------------------------------------------------------- walk
 
-  // grid records are streamed past the caches unless their SHA-1 prefixes
-  // are filled in after the grid SHA-1 lands (fill_grid_records)
-  bool stream_recs() const {
-    static const bool cached = getenv("ZC_REC_CACHED") != nullptr;  // TEMP (round-5 A/B)
-    return !(pre_sha_n_ && cached);
-  }
   // the runs of records fill_grid_records wrote since the last finalize:
   // records rec0 .. rec0 + n - 1 are [off0 + j W, off0 + (j + 1) W), one kind;
   // finalize_records classifies them without reading them back
@@ -2060,7 +2054,7 @@ class Resolver {
     const uint8_t* dead = indexable_ ? dead_.data() + nconf_ : nullptr;
     if (ndead_ == 0 && r_e_ + ks_ * W_ >= s_ && kmax - ks_ >= kParallelRecords) {
       // every chunk of the run is saved: record o + j is grid chunk ks_ + j
-      fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr, stream_recs());
+      fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr);
       gruns_.push_back({o, kmax - ks_, r_e_ + ks_ * W_, kind});
       s_ = r_e_ + kmax * W_;
       ks_ = kmax;
@@ -2123,7 +2117,7 @@ class Resolver {
     if (!nchain) return;
     const size_t o = c_.recs.size();
     c_.recs.resize(o + nchain);
-    fill_grid_records(c_.recs.data() + o, nchain, r_e_, j + 1, W_, ZC_CHUNK_DUP, c_.h_key.p, stream_recs());
+    fill_grid_records(c_.recs.data() + o, nchain, r_e_, j + 1, W_, ZC_CHUNK_DUP, c_.h_key.p);
     gruns_.push_back({o, nchain, r_e_ + (j + 1) * W_, (uint32_t)ZC_CHUNK_DUP});
     r_ = r_e_ + (uint64_t)jn * W_;
     s_ = r_;
@@ -2322,16 +2316,6 @@ class Resolver {
   // 0.1).  After the batch the walk, the records and the index registration
   // run on the host while the SHA-1 does.
   bool sha_pending_ = false;
-  // ZC_SHA_AT=1 (A/B): the grid SHA-1 queued right behind the scan, beside
-  // the first epoch's batch (its latency-bound kernels run at wave priority 3,
-  // ZC_URGENT); 0: behind the batch
-  static bool sha_behind_scan() {
-    static const int v = [] {
-      const char* e = getenv("ZC_SHA_AT");
-      return e ? atoi(e) : 0;
-    }();
-    return v == 1;
-  }
   void pre_sha() {
     pre_sha_n_ = 0;
     gsha_ready_ = false;
@@ -2359,7 +2343,13 @@ class Resolver {
   // ---------------------------------------------------------------- finalize
   // Records [nrec_done, size) are complete once their pieces have digests
   // and (ZC_FLAG_SHA1) every chunk record its SHA-1 prefix.
-  std::vector<uint64_t> fresh_;  // NEW W-byte chunks of the stream still resident: offset,
+  // finalize_records' per-record lists and the stream's new chunks live in the
+  // context, so their capacity carries over from stream to stream (a fresh
+  // 1 MB vector per stream is new pages, whose first touch faulted in ~0.5 ms)
+  std::vector<uint64_t>& gq_ = c_.fin_gq;
+  std::vector<uint32_t>& gslot_ = c_.fin_gslot;
+  std::vector<uint32_t>& frec_ = c_.fin_frec;
+  std::vector<uint64_t>& fresh_ = c_.fin_fresh;  // NEW W-byte chunks of the stream still resident: offset,
   std::vector<uint8_t, DefaultInit<uint8_t>> fresh_sha_;  // and SHA-1 prefix (ZC_FLAG_SHA1)
   // stream_end: the stream's end (run_final): with ZC_FLAG_SHA1 its new W-byte
   // chunks join the context's index here, their device metadata queued before
@@ -2388,7 +2378,6 @@ class Resolver {
     std::vector<uint64_t> h = range_digests(a, b);
     for (size_t j = 0; j < rest.size(); ++j) c_.recs[need_digest_[rest[j]].rec].rolling = h[j];
     need_digest_.clear();
-    const double t_dig = ms_since(t0);
     const size_t r0 = c_.nrec_done, r1 = c_.recs.size();
     const bool sha1 = c_.flags & ZC_FLAG_SHA1;
     struct ClearRuns {
@@ -2413,16 +2402,19 @@ class Resolver {
     std::vector<uint64_t> sa;
     std::vector<uint32_t> sl;
     std::vector<size_t> idx;
-    std::vector<uint64_t> gq;    // grid-chunk records: record index << 32 | chunk (both < 2^32)
-    std::vector<uint32_t> gslot;  // per gq entry: its fresh_ entry (from f0), or kNoSlot
-    std::vector<uint32_t> frec;  // record (from r0) of each new fresh_ entry
+    std::vector<uint64_t>& gq = gq_;        // grid-chunk records: record index << 32 | chunk (both < 2^32)
+    std::vector<uint32_t>& gslot = gslot_;  // per gq entry: its fresh_ entry (from f0), or kNoSlot
+    std::vector<uint32_t>& frec = frec_;    // record (from r0) of each new fresh_ entry
+    gq.clear();
+    gslot.clear();
+    frec.clear();
     std::vector<uint32_t> fsh;   // fresh_ entries (from f0) hashed here (not grid chunks): their idx entry
     constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
     const size_t f0 = fresh_.size();
     gq.reserve(r1 - r0);
     gslot.reserve(r1 - r0);
     frec.reserve(r1 - r0);
-    fresh_.reserve(fresh_.size() + (r1 - r0));
+    if (fresh_.capacity() < fresh_.size() + (r1 - r0)) fresh_.reserve(2 * (fresh_.size() + (r1 - r0)));
     size_t gr = 0;
     while (gr < gruns_.size() && gruns_[gr].rec0 < r0) ++gr;
     for (size_t i = r0; i < r1; ++i) {
@@ -2471,7 +2463,6 @@ class Resolver {
       sl.push_back(r.size);
       idx.push_back(i);
     }
-    const double t_class = ms_since(t0);
     std::vector<uint8_t> sh = sha1s(sa, sl);
     HistPending hp;
     auto th = Clock::now();
@@ -2499,7 +2490,6 @@ class Resolver {
     const uint8_t* gsha = pre_sha_n_ ? grid_sha() : nullptr;  // waits for the side stream
     c_.stats.sha_wait_ms += ms_since(tw);
     auto tf = Clock::now();
-    const size_t npairs = spec_pairs_.size();
     {
       // the speculated joins (epoch): every pair's prefixes must agree
       std::atomic<bool> refuted{false};
@@ -2537,8 +2527,7 @@ class Resolver {
       }
       _mm_sfence();
     };
-    int mine = -1;
-    if (team) mine = SpinTeam::get().run(gq.size(), fill);
+    if (team) SpinTeam::get().run(gq.size(), fill);
     else fill(0, gq.size());
     for (size_t j = 0; j < idx.size(); ++j) memcpy(c_.recs[idx[j]].sha1, &sh[j * 20], 16);
     for (uint32_t t : fsh) {  // new chunks hashed here: their slot is their place among frec
@@ -2546,16 +2535,9 @@ class Resolver {
       const size_t slot = std::lower_bound(frec.begin(), frec.end(), rec) - frec.begin();
       memcpy(fs + 16 * slot, &sh[t * 20], 16);
     }
-    const double t_fill = ms_since(tf);
     c_.nrec_done = r1;
     if (stream_end) stream_end_index(&hp, in_place, &hp_ancless);
     c_.stats.sha_fill_ms += ms_since(tf);
-    if (getenv("ZC_DEBUG_FILL"))  // TEMP (round-5 measurement)
-      fprintf(stderr,
-              "digests %.3f classify %.3f hist %.3f wait %.3f checks+fill %.3f (main did %d parts) end %.3f (gq %zu "
-              "frec %zu pairs %zu)\n",
-              t_dig, t_class - t_dig, ms_since(th) - ms_since(tw), ms_since(tw) - ms_since(tf), t_fill, mine,
-              ms_since(tf) - t_fill, gq.size(), frec.size(), npairs);
   }
 
   // The stream's end.  With ZC_FLAG_SHA1 its new W-byte chunks join the
