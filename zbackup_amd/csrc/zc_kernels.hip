@@ -85,15 +85,32 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total
 
 // Rabin-Karp accumulator (no leading 257^len term) of bytes [a, b):
 // sum_i data[i] * 257^(b-1-i) mod 2^64, folding whole spans from blk[].
+// acc * 257^(b - a) + the bytes [a, b) Horner-folded (mod 2^64): bytes up to a
+// 16-byte boundary one at a time, then 16-byte loads folded two bytes per
+// step (acc * 257^2 + 257 b_0 + b_1), then the rest one at a time.  (The
+// stream base is 16-byte aligned, so absolute offsets give the alignment.)
+__device__ __forceinline__ uint64_t rk_bytes(const uint8_t* __restrict__ data, uint64_t acc, uint64_t a, uint64_t b) {
+  for (; a < b && (a & 15); ++a) acc = acc * 257u + data[a];
+  for (; a + 16 <= b; a += 16) {
+    const uint4 v = *(const uint4*)(data + a);
+    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t x = xs[d];
+      acc = acc * 66049u + ((x & 0xFFu) * 257u + ((x >> 8) & 0xFFu));
+      acc = acc * 66049u + (((x >> 16) & 0xFFu) * 257u + (x >> 24));
+    }
+  }
+  for (; a < b; ++a) acc = acc * 257u + data[a];
+  return acc;
+}
+
 __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk,
                            uint64_t a, uint64_t b) {
   uint64_t acc = 0;
   uint64_t a_up = (a + ZC_SPAN - 1) / ZC_SPAN * ZC_SPAN;
-  if (a_up >= b) {
-    for (uint64_t i = a; i < b; ++i) acc = acc * 257u + data[i];
-    return acc;
-  }
-  for (uint64_t i = a; i < a_up; ++i) acc = acc * 257u + data[i];
+  if (a_up >= b) return rk_bytes(data, 0, a, b);
+  acc = rk_bytes(data, 0, a, a_up);
   uint64_t b_dn = b / ZC_SPAN * ZC_SPAN;
   const uint64_t m = span_mul();
   uint64_t k = a_up / ZC_SPAN;
@@ -126,8 +143,7 @@ __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __r
     k += 8;
   }
   for (; k < k1; ++k) acc = acc * m + blk[k];
-  for (uint64_t i = b_dn; i < b; ++i) acc = acc * 257u + data[i];
-  return acc;
+  return rk_bytes(data, acc, b_dn, b);
 }
 
 __device__ uint32_t rk_acc32(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk,
@@ -2290,6 +2306,22 @@ constexpr uint64_t kKey64FilterMax = 64;  // longer runs are left to the walk
 // thread per screen run: a short run keeps only [first, last] of the
 // positions whose 64-bit window key (257^W + the window's accumulator) is
 // in the sets; none: the run becomes empty
+// Bloom-mode runs of at most kKey64FilterMax positions, trimmed to the
+// positions whose exact 64-bit key is in the set (the runs' first and last
+// hits; none: the run is emptied).  Runs of up to kKey64LaneMax positions
+// take a lane each (zc_key64_filter_kernel: most runs are a false Bloom hit
+// or two); longer ones a wave each, one position per lane
+// (zc_key64_filter_wave_kernel), so no lane walks 64 positions in turn.
+constexpr uint64_t kKey64LaneMax = 8;
+__device__ __forceinline__ void key64_trim(Run* __restrict__ runs, uint64_t i, const Run& r, uint64_t first,
+                                           uint64_t last) {
+  if (first == ~0ull) {
+    runs[i].end = r.start;
+  } else {
+    runs[i].start = first;
+    runs[i].end = last + 1;
+  }
+}
 __global__ void __launch_bounds__(64) zc_key64_filter_kernel(const uint8_t* __restrict__ data,
                                                              const uint64_t* __restrict__ blk, uint32_t W, uint64_t pw,
                                                              Run* __restrict__ runs, uint64_t nruns,
@@ -2297,27 +2329,38 @@ __global__ void __launch_bounds__(64) zc_key64_filter_kernel(const uint8_t* __re
                                                              int zero_key, const uint64_t* __restrict__ list,
                                                              uint32_t nl) {
   ZC_URGENT();
-  // one wave per run, one position per lane (a run is at most 64 positions):
-  // each lane's exact key is an independent fold, so the wave computes the
-  // run's keys side by side instead of one lane walking them in turn
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nruns) return;
+  const Run r = runs[i];
+  if (r.end - r.start > kKey64LaneMax) return;
+  uint64_t first = ~0ull, last = 0;
+  for (uint64_t p = r.start; p < r.end; ++p)
+    if (key64_in(pw + rk_acc(data, blk, p + 1 - W, p + 1), set, sbits, zero_key, list, nl)) {
+      if (first == ~0ull) first = p;
+      last = p;
+    }
+  key64_trim(runs, i, r, first, last);
+}
+__global__ void __launch_bounds__(64) zc_key64_filter_wave_kernel(const uint8_t* __restrict__ data,
+                                                                  const uint64_t* __restrict__ blk, uint32_t W,
+                                                                  uint64_t pw, Run* __restrict__ runs, uint64_t nruns,
+                                                                  const uint64_t* __restrict__ set, uint32_t sbits,
+                                                                  int zero_key, const uint64_t* __restrict__ list,
+                                                                  uint32_t nl) {
+  ZC_URGENT();
   static_assert(kKey64FilterMax <= 64, "a lane per position");
   const uint64_t i = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (i >= nruns) return;
   const Run r = runs[i];
-  if (r.end - r.start > kKey64FilterMax) return;
+  if (r.end - r.start <= kKey64LaneMax || r.end - r.start > kKey64FilterMax) return;
   const uint64_t p = r.start + lane;
   bool hit = false;
   if (p < r.end) hit = key64_in(pw + rk_acc(data, blk, p + 1 - W, p + 1), set, sbits, zero_key, list, nl);
   const uint64_t m = __ballot(hit);
-  if (lane == 0) {
-    if (!m) {
-      runs[i].end = r.start;
-    } else {
-      runs[i].start = r.start + (uint64_t)__builtin_ctzll(m);
-      runs[i].end = r.start + 64 - (uint64_t)__builtin_clzll(m);
-    }
-  }
+  if (lane == 0)
+    key64_trim(runs, i, r, m ? r.start + (uint64_t)__builtin_ctzll(m) : ~0ull,
+               m ? r.start + 63 - (uint64_t)__builtin_clzll(m) : 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2855,8 +2898,10 @@ hipError_t launch_key64_filter(const uint8_t* data, const uint64_t* blk, uint32_
                                const uint64_t* list, uint32_t nl, hipStream_t s) {
   if (!nruns) return hipSuccess;
   if (nruns > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(zc_key64_filter_kernel, dim3((unsigned)nruns), dim3(64), 0, s, data, blk, W, pw, runs, nruns, set,
-                     sbits, zero_key, list, nl);
+  hipLaunchKernelGGL(zc_key64_filter_kernel, dim3(blocks_for(nruns, 64)), dim3(64), 0, s, data, blk, W, pw, runs,
+                     nruns, set, sbits, zero_key, list, nl);
+  hipLaunchKernelGGL(zc_key64_filter_wave_kernel, dim3((unsigned)nruns), dim3(64), 0, s, data, blk, W, pw, runs,
+                     nruns, set, sbits, zero_key, list, nl);
   return hipGetLastError();
 }
 
