@@ -89,7 +89,12 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total
 // 16-byte boundary one at a time, then 16-byte loads folded two bytes per
 // step (acc * 257^2 + 257 b_0 + b_1), then the rest one at a time.  (The
 // stream base is 16-byte aligned, so absolute offsets give the alignment.)
+template <bool kVec = true>
 __device__ __forceinline__ uint64_t rk_bytes(const uint8_t* __restrict__ data, uint64_t acc, uint64_t a, uint64_t b) {
+  if (!kVec) {
+    for (; a < b; ++a) acc = acc * 257u + data[a];
+    return acc;
+  }
   for (; a < b && (a & 15); ++a) acc = acc * 257u + data[a];
   for (; a + 16 <= b; a += 16) {
     const uint4 v = *(const uint4*)(data + a);
@@ -105,12 +110,17 @@ __device__ __forceinline__ uint64_t rk_bytes(const uint8_t* __restrict__ data, u
   return acc;
 }
 
+// (kVec = false: the edges one byte at a time -- for the screen kernels, whose
+// lane start states need no edges at W = 0 mod 1 KiB and whose register
+// allocation the vector edge loop disturbed: the two-level screen ran 2.5 ->
+// 3.7 ms per GiB with it inlined, round 5)
+template <bool kVec = true>
 __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk,
                            uint64_t a, uint64_t b) {
   uint64_t acc = 0;
   uint64_t a_up = (a + ZC_SPAN - 1) / ZC_SPAN * ZC_SPAN;
-  if (a_up >= b) return rk_bytes(data, 0, a, b);
-  acc = rk_bytes(data, 0, a, a_up);
+  if (a_up >= b) return rk_bytes<kVec>(data, 0, a, b);
+  acc = rk_bytes<kVec>(data, 0, a, a_up);
   uint64_t b_dn = b / ZC_SPAN * ZC_SPAN;
   const uint64_t m = span_mul();
   uint64_t k = a_up / ZC_SPAN;
@@ -143,7 +153,7 @@ __device__ uint64_t rk_acc(const uint8_t* __restrict__ data, const uint64_t* __r
     k += 8;
   }
   for (; k < k1; ++k) acc = acc * m + blk[k];
-  return rk_bytes(data, acc, b_dn, b);
+  return rk_bytes<kVec>(data, acc, b_dn, b);
 }
 
 __device__ uint32_t rk_acc32(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk,
@@ -1529,7 +1539,7 @@ __global__ void __launch_bounds__(ZC_TPB) zc_fscan_kernel(
   // (Bloom mode, large key sets) mod 2^64 against the 64-bit Bloom filter
   const uint64_t pw64 = bloom ? pow257_dev(W) : 0;
   auto fstart = [&](uint64_t a, uint64_t b) -> uint64_t {
-    return bloom ? rk_acc(data, blk, a, b) : (uint64_t)rk_acc32(data, blk, a, b);
+    return bloom ? rk_acc<false>(data, blk, a, b) : (uint64_t)rk_acc32(data, blk, a, b);
   };
   auto fstep = [&](uint64_t v, uint32_t bi, uint32_t bo) -> uint64_t {
     return bloom ? v * 257u + bi - (uint64_t)bo * pw64 : (uint64_t)((uint32_t)v * 257u + bi - bo * pw32);
@@ -1918,7 +1928,7 @@ __global__ void __launch_bounds__(kFTPBn<NF>, 1) zc_fscan_staged_kernel(
           carry = make_uint4(w[0], w[1], w[2], w[3]);
         }
       }
-      if constexpr (NF >= 64) V64 = ps < n ? rk_acc(data, blk, ps >= W ? ps - W : 0, ps) : 0;
+      if constexpr (NF >= 64) V64 = ps < n ? rk_acc<false>(data, blk, ps >= W ? ps - W : 0, ps) : 0;
       head = wtbase < (uint64_t)W + 16;
       need_valid = wtbase < p_start || wtbase + ZC_FWT > p_end;
       open = false;
