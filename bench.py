@@ -596,7 +596,8 @@ def run_rank(args):
                 b5.close()
                 inc[label] = {"value": round(job_value(n, world, 1, job_max(min(ts), world)), 3), "unit": "GiB/s",
                               "ms": round(min(ts) * 1e3, 3), "dup_records": int((kinds == 1).sum()),
-                              "new_records": int((kinds == 0).sum()), "hist_entries": st5["hist_entries"]}
+                              "new_records": int((kinds == 0).sum()), "hist_entries": st5["hist_entries"],
+                              "stages": stage_dict(st5)}
             del other
             extras["incremental"] = inc
         # the stream starts in (pinned) host memory, as in zutils.cc:100-124:

@@ -196,3 +196,38 @@ def test_respeculation_on_a_context_with_history_and_seeds(torch_cuda, W):
             assert bc.record_tuples() == want, i
             assert bc.stats()["respeculations"] == (1 if i == 1 else 0), i
             bc.reset()
+
+
+@pytest.mark.parametrize("W", [4096, 65536])
+def test_historic_grid_key_collision_refutes_speculation(torch_cuda, W):
+    # stream a saves C1 as a grid chunk (it joins the historic index); stream b
+    # holds C2 (C1's key, other bytes) as a grid chunk, and no in-stream pair:
+    # on the device path C2's window is joined to C1's historic entry on the
+    # key before the grid SHA-1 exists, the join is refuted when the digests
+    # land and the stream is redone exactly -- C2 saved as new.  Stream c then
+    # repeats C1 on its grid: joined the same way, confirmed, a duplicate.
+    from zbackup_amd import BackupCreator
+    c1, c2 = _tm_pair(W, 16)
+    a = np.concatenate([_rand(2 * W, 61), c1, _rand(W, 62)])
+    b = np.concatenate([_rand(3 * W, 63), c2, _rand(W + 11, 65)])
+    c = np.concatenate([_rand(W, 66), c1, _rand(2 * W + 3, 67)])
+    want_a = oracle.chunk(a, W)
+    idx = [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in want_a if k == "N" and s == W]
+    want_b = oracle.chunk(b, W, seeds=idx)
+    idx += [(bytes.fromhex(sha), h, s) for (k, o, s, h, sha) in want_b if k == "N" and s == W]
+    want_c = oracle.chunk(c, W, seeds=idx)
+    assert [r[0] for r in _at(want_b, 3 * W)] == ["N"] and [r[0] for r in _at(want_c, W)] == ["D"]
+    with BackupCreator(W, sha1=True) as bc:
+        ta = torch_cuda.from_numpy(a).to("cuda")
+        bc.chunk_device(ta.data_ptr(), a.size)
+        assert bc.record_tuples() == want_a
+        bc.reset()
+        tb = torch_cuda.from_numpy(b).to("cuda")
+        bc.chunk_device(tb.data_ptr(), b.size)
+        assert bc.record_tuples() == want_b
+        assert bc.stats()["respeculations"] == 1
+        bc.reset()
+        tc = torch_cuda.from_numpy(c).to("cuda")
+        bc.chunk_device(tc.data_ptr(), c.size)
+        assert bc.record_tuples() == want_c
+        assert bc.stats()["respeculations"] == 0

@@ -1445,6 +1445,16 @@ class Resolver {
         if (key[j] == c_.hkey[hc[hidx[j]].ref]) {
           // a window that is a grid chunk has its SHA-1 from the speculative
           // grid pass (the incremental backup of unchanged data: all of them)
+          if (spec_ && grid_sha_pending(ha[j])) {
+            // speculatively (whole-stream SHA-1 mode): joined on the key now,
+            // the SHA-1 prefixes compared once the grid digests land
+            // (finalize_records; a mismatch redoes the stream without
+            // speculation), so the walk need not wait for the grid SHA-1
+            const uint64_t i = hidx[j];
+            hcands_.push_back({hc[i].p, hc[i].ref});
+            spec_hist_.push_back({ha[j] / W_, hc[i].ref});
+            continue;
+          }
           if (const uint8_t* g = grid_sha_of(ha[j])) {
             const uint64_t i = hidx[j];
             if (memcmp(g, &c_.hsha[16 * (size_t)hc[i].ref], 16) == 0) hcands_.push_back({hc[i].p, hc[i].ref});
@@ -2288,6 +2298,9 @@ class Resolver {
   // speculative SHA-1 class joins (whole-stream runs): the pairs of grid
   // chunks joined before their digests existed
   std::vector<std::pair<uint64_t, uint64_t>> spec_pairs_;
+  // speculative historic joins: {grid chunk, historic entry} whose keys are
+  // equal, joined before the chunk's digest existed
+  std::vector<std::pair<uint64_t, uint64_t>> spec_hist_;
  public:
   bool spec_ = false;
  private:
@@ -2298,6 +2311,10 @@ class Resolver {
       gsha_ready_ = true;
     }
     return c_.h_gsha.p;
+  }
+  // window [ws, ws + W) is a grid chunk whose SHA-1 the side stream computes
+  bool grid_sha_pending(uint64_t ws) const {
+    return pre_sha_n_ && ws % W_ == 0 && ws / W_ < pre_sha_n_ && ws + W_ <= n_;
   }
   // grid chunk q's SHA-1 when window [ws, ws + W) is that chunk, else null
   const uint8_t* grid_sha_of(uint64_t ws) {
@@ -2502,6 +2519,38 @@ class Resolver {
       };
       if (spec_pairs_.size() >= kParallelRecordsMin) SpinTeam::get().run(spec_pairs_.size(), check);
       else check(0, spec_pairs_.size());
+      // the speculated historic joins: a window joined on the key to several
+      // entries (a key chain, chunk_index.cc:119-143) is right when ANY of them
+      // has its prefix; a window with none refutes the speculation
+      std::mutex mm;
+      std::vector<size_t> miss;
+      auto check_hist = [&](size_t a, size_t b) {
+        std::vector<size_t> mine;
+        for (size_t j = a; j < b; ++j)
+          if (memcmp(gsha + 20 * spec_hist_[j].first, &c_.hsha[16 * (size_t)spec_hist_[j].second], 16) != 0)
+            mine.push_back(j);
+        if (!mine.empty()) {
+          std::lock_guard<std::mutex> lk(mm);
+          miss.insert(miss.end(), mine.begin(), mine.end());
+        }
+      };
+      if (spec_hist_.size() >= kParallelRecordsMin) SpinTeam::get().run(spec_hist_.size(), check_hist);
+      else check_hist(0, spec_hist_.size());
+      if (miss.size() > 64) {
+        refuted.store(true);  // (many wrong-prefix chain entries: redone exactly rather than searched)
+      } else {
+        for (size_t j : miss) {
+          const uint64_t q = spec_hist_[j].first;
+          bool any = false;
+          for (const auto& sp : spec_hist_)
+            if (sp.first == q && memcmp(gsha + 20 * q, &c_.hsha[16 * (size_t)sp.second], 16) == 0) {
+              any = true;
+              break;
+            }
+          if (!any) refuted.store(true);
+        }
+      }
+      spec_hist_.clear();
       if (refuted.load()) throw Respeculate{};
       spec_pairs_.clear();
     }
