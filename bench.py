@@ -581,16 +581,23 @@ def run_rank(args):
             fill_stream(torch, other, n, args.config, seed + 1000003, local)
             inc = {}
             for label, first in (("same_stream_again", buf), ("after_other_stream", other)):
-                b5 = BackupCreator(W64, device=local, sha1=True, timing=True)
-                b5.chunk_device(first.data_ptr(), n)
-                torch.cuda.synchronize()
-                reps = 3 if label == "same_stream_again" else 1
+                # same data again: 3 repeats on one context (nothing new joins
+                # the index); after another stream: each repeat on a fresh
+                # context (the measured stream adds 131,072 entries)
                 ts = []
-                for _ in range(reps):
+                b5 = None
+                for rep in range(3):
+                    if b5 is None:
+                        b5 = BackupCreator(W64, device=local, sha1=True, timing=True)
+                        b5.chunk_device(first.data_ptr(), n)
+                        torch.cuda.synchronize()
                     t1 = time.perf_counter()
                     b5.chunk_device(buf.data_ptr(), n)
                     torch.cuda.synchronize()
                     ts.append(time.perf_counter() - t1)
+                    if label == "after_other_stream" and rep < 2:
+                        b5.close()
+                        b5 = None
                 st5 = b5.stats()
                 kinds = b5.records()["kind"]
                 b5.close()
