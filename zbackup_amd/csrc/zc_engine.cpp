@@ -343,6 +343,13 @@ class Resolver;
 // an epoch's own anchorless keys (grown when an epoch brings more)
 constexpr uint64_t kChkRoomDefault = 65536;
 
+// a candidate window of the walk: the window ending at p equals ref (an epoch
+// ref or a historic entry)
+struct CandPos {
+  uint64_t p;
+  uint32_t ref;
+};
+
 }  // namespace
 
 struct zc_ctx {
@@ -411,9 +418,20 @@ struct zc_ctx {
   // being cut.  The taken prefix is dropped once it is most of the vector, so
   // draining a long stream in small batches stays linear.
   std::vector<zc_record, DefaultInit<zc_record>> recs;  // resize leaves new records to be written
-  // the resolver's per-stream lists, kept here for their capacity (Resolver)
+  // the resolver's per-stream lists, kept here for their capacity (Resolver):
+  // a list built fresh per stream is new pages, and an incremental backup's
+  // candidate lists are megabytes
   std::vector<uint64_t> fin_gq, fin_fresh;
   std::vector<uint32_t> fin_gslot, fin_frec;
+  std::vector<CandPos> res_acands, res_hcands, res_sort_tmp;
+  std::vector<std::pair<uint64_t, uint64_t>> res_spec_hist;
+  std::vector<uint64_t> res_ha, res_hidx;
+  std::vector<uint8_t> res_ok;
+  // the probe's candidates, read back into pinned memory: a large copy into
+  // pageable memory is staged by pinning the caller's pages, and freeing such
+  // pages later (the list's destructor) stalled the next call's first
+  // submission by 8-28 ms on the GPU box
+  HostBuf<Cand> h_cand;
   size_t nrec_done = 0;
   size_t rec_head = 0;
   // every entry point holds this: calls on one context from several threads
@@ -663,6 +681,9 @@ class Resolver {
     r_ = s_ = x_resume_ = hspan_ = 0;
     gruns_.clear();
     fresh_.clear();
+    spec_hist_.clear();
+    acands_.clear();
+    hcands_.clear();
     scan_setup();
   }
   // bytes [0, n) of the stream are (being) copied to the device, in order on
@@ -1045,12 +1066,9 @@ class Resolver {
   uint64_t f_min_vis_ = kInf;
   bool has_f_ = false;
 
-  struct ACand {
-    uint64_t p;
-    uint32_t ref;
-  };
-  std::vector<ACand> acands_;
-  std::vector<ACand> hcands_;  // confirmed candidates of historic entries (ref = entry)
+  using ACand = CandPos;
+  std::vector<ACand>& acands_ = c_.res_acands;
+  std::vector<ACand>& hcands_ = c_.res_hcands;  // confirmed candidates of historic entries (ref = entry)
 
   // F verification batch (positions ascending)
   struct FBatch {
@@ -1407,22 +1425,25 @@ class Resolver {
   // as ChunkIndex::findChunk confirms them (chunk_index.cc:119-143)
   void verify_candidates(uint64_t nc) {
     c_.stats.candidates += nc;
-    std::vector<Cand> hc(nc);
-    d2h(c_, hc.data(), c_.cand.p, nc);
+    c_.h_cand.ensure(nc);
+    const Cand* const hc = c_.h_cand.p;
+    d2h(c_, c_.h_cand.p, c_.cand.p, nc);
     sync(c_);
     // a window that is exactly a grid chunk of this epoch in the candidate's
     // class is already known equal (the class was byte-verified)
     std::vector<uint64_t> wa, ra;
     std::vector<uint64_t> idx;
-    std::vector<uint8_t> ok(nc, 1);
-    std::vector<uint64_t> ha, hb;
-    std::vector<uint64_t> hidx;
+    std::vector<uint8_t>& ok = c_.res_ok;
+    ok.assign(nc, 1);
+    std::vector<uint64_t>& ha = c_.res_ha;  // historic candidates' windows [ha, ha + W)
+    std::vector<uint64_t>& hidx = c_.res_hidx;
+    ha.clear();
+    hidx.clear();
     for (uint64_t i = 0; i < nc; ++i) {
       const uint64_t ws = hc[i].p - W_ + 1;
       if (hc[i].pad) {
         ok[i] = 0;
         ha.push_back(ws);
-        hb.push_back(ws + W_);
         hidx.push_back(i);
         continue;
       }
@@ -1437,7 +1458,9 @@ class Resolver {
     std::vector<uint8_t> vok = verify_pairs(wa, ra, W_);
     for (size_t j = 0; j < idx.size(); ++j) ok[idx[j]] = vok[j];
     if (!hidx.empty()) {
-      const std::vector<uint64_t> key = range_digests(ha, hb);
+      const uint64_t* const key = window_digests(ha);
+      hcands_.reserve(hcands_.size() + hidx.size());
+      if (spec_) spec_hist_.reserve(spec_hist_.size() + hidx.size());
       std::vector<uint64_t> sa;
       std::vector<uint32_t> sl;
       std::vector<size_t> sidx;
@@ -1489,7 +1512,8 @@ class Resolver {
   void sort_by_position(std::vector<ACand>& v) {
     const size_t m = v.size();
     if (m < 2) return;
-    std::vector<ACand> tmp(m);
+    std::vector<ACand>& tmp = c_.res_sort_tmp;
+    tmp.resize(m);
     uint32_t bits = 1;
     while (bits < 64 && (n_ >> bits)) ++bits;
     std::vector<uint32_t> cnt(2048);
@@ -1542,6 +1566,28 @@ class Resolver {
     sync(c_);
     memcpy(out.data(), c_.h_rout.p, nr * sizeof(uint64_t));
     return out;
+  }
+
+  // RollingHash digests of the W-byte windows [a[i], a[i] + W), in pinned
+  // memory (valid until the next range digest)
+  const uint64_t* window_digests(const std::vector<uint64_t>& a) {
+    const size_t nr = a.size();
+    c_.va.ensure(nr);
+    c_.vb.ensure(nr);
+    c_.dout.ensure(nr);
+    c_.h_ra.ensure(nr);
+    c_.h_rb.ensure(nr);
+    c_.h_rout.ensure(nr);
+    for (size_t i = 0; i < nr; ++i) {
+      c_.h_ra.p[i] = a[i];
+      c_.h_rb.p[i] = a[i] + W_;
+    }
+    h2d(c_, c_.va.p, c_.h_ra.p, nr);
+    h2d(c_, c_.vb.p, c_.h_rb.p, nr);
+    HCK(launch_range_digest(d_, n_, blk_v(), c_.va.p, c_.vb.p, (uint32_t)nr, c_.dout.p, c_.stream));
+    d2h(c_, c_.h_rout.p, c_.dout.p, nr);
+    sync(c_);
+    return c_.h_rout.p;
   }
 
   std::vector<uint8_t> sha1s(const std::vector<uint64_t>& a, const std::vector<uint32_t>& len) {
@@ -2300,7 +2346,7 @@ class Resolver {
   std::vector<std::pair<uint64_t, uint64_t>> spec_pairs_;
   // speculative historic joins: {grid chunk, historic entry} whose keys are
   // equal, joined before the chunk's digest existed
-  std::vector<std::pair<uint64_t, uint64_t>> spec_hist_;
+  std::vector<std::pair<uint64_t, uint64_t>>& spec_hist_ = c_.res_spec_hist;
  public:
   bool spec_ = false;
  private:
