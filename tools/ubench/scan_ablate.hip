@@ -25,9 +25,10 @@ int main(int argc, char** argv) {
   const PoolOut po{dbase, dcnt, prel, pg, wcap, 0};
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   struct V { const char* name; void (*k)(const uint8_t*, uint64_t, uint64_t, uint64_t, int32_t, uint64_t*, PoolOut, unsigned long long*); std::vector<float> t; };
+  // k == nullptr: the product kernel through its launcher (its own geometry)
   constexpr int P = kAblProduct;
   std::vector<V> vs = {
-    {"product zc_scan_kernel", zc_scan_kernel, {}},
+    {"product zc_scan_kernel", nullptr, {}},
     {"ablation copy, product bits", abl_scan_kernel<P>, {}},
     {"no_atomic", abl_scan_kernel<P | ABL_NO_ATOMIC>, {}},
     {"te_no_anchor_store", abl_scan_kernel<P | ABL_TE_NO_ANCHOR_STORE>, {}},
@@ -38,7 +39,8 @@ int main(int argc, char** argv) {
     for (auto& v : vs) {
       CK(hipMemset(cnt, 0, 64));
       CK(hipEventRecord(a));
-      hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, (uint64_t)0, ntiles, anchor_lo_for(65536), blk, po, cnt);
+      if (!v.k) CK(launch_scan_tiles(d, n, 0, ntiles, anchor_lo_for(65536), blk, po, cnt, 0));
+      else hipLaunchKernelGGL(v.k, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n, (uint64_t)0, ntiles, anchor_lo_for(65536), blk, po, cnt);
       CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
       float ms; CK(hipEventElapsedTime(&ms, a, b));
       if (round) v.t.push_back(ms);

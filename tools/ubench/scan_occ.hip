@@ -171,13 +171,13 @@ int main(int argc, char** argv) {
   const PoolOut po{dbase, dcnt, prel, pg, wcap, 0};
   struct V { const char* name; OccK k; int tpb; int wg_per_cu; std::vector<float> t; uint64_t sig; unsigned long long pool; };
   std::vector<V> vs = {
-    {"product zc_scan_kernel (8 waves, ring 2)", nullptr, ZC_SCAN_TPB, 1, {}, 0, 0},
+    {"product zc_scan_kernel", nullptr, ZC_SCAN_TPB, 1, {}, 0, 0},
     {"per-wave tiles, 8 waves x1, ring 2, wpe1", occ_scan_kernel<8, 2, 1>, 512, 1, {}, 0, 0},
-    {"per-wave tiles, 8 waves x1, ring 1, wpe1", occ_scan_kernel<8, 1, 1>, 512, 1, {}, 0, 0},
-    {"per-wave tiles, 4 waves x2, ring 1, wpe1", occ_scan_kernel<4, 1, 1>, 256, 2, {}, 0, 0},
     {"per-wave tiles, 4 waves x3, ring 1, wpe3", occ_scan_kernel<4, 1, 3>, 256, 3, {}, 0, 0},
+    {"product zc_scan_kernel (again)", nullptr, ZC_SCAN_TPB, 1, {}, 0, 0},
     {"per-wave tiles, 2 waves x6, ring 1, wpe3", occ_scan_kernel<2, 1, 3>, 128, 6, {}, 0, 0},
-    {"per-wave tiles, 1 wave x12, ring 1, wpe3", occ_scan_kernel<1, 1, 3>, 64, 12, {}, 0, 0},
+    {"per-wave tiles, 8 waves x1, ring 2 (again)", occ_scan_kernel<8, 2, 1>, 512, 1, {}, 0, 0},
+    {"per-wave tiles, 4 waves x3, ring 1 (again)", occ_scan_kernel<4, 1, 3>, 256, 3, {}, 0, 0},
   };
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   std::vector<uint32_t> h32(n / ZC_SPAN * 2), hc(nwt);
@@ -186,8 +186,7 @@ int main(int argc, char** argv) {
       CK(hipMemset(cnt, 0, 128));
       CK(hipEventRecord(a));
       if (!v.k)
-        hipLaunchKernelGGL(zc_scan_kernel, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0, d, n,
-                           (uint64_t)0, ntiles, lo, blk, po, cnt);
+        CK(launch_scan_tiles(d, n, 0, ntiles, lo, blk, po, cnt, 0));
       else
         hipLaunchKernelGGL(v.k, dim3(cus * v.wg_per_cu), dim3(v.tpb), 0, 0, d, n, nwt, lo, blk, po, cnt);
       if (hipError_t e = hipGetLastError(); e != hipSuccess) {

@@ -259,8 +259,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&b));
   auto runA = [&]() {
     hipMemsetAsync(cnt, 0, 64, 0);
-    hipLaunchKernelGGL(zc_scan_kernel, dim3(std::min<uint64_t>(ntiles, cus)), dim3(ZC_SCAN_TPB), 0, 0,
-                       d, n, (uint64_t)0, ntiles, lo, blkA, po, cnt);
+    (void)launch_scan_tiles(d, n, 0, ntiles, lo, blkA, po, cnt, 0);
   };
   // wpc: workgroups of 8 waves per CU (no LDS ring: up to 4 waves per SIMD fit 119 VGPRs)
   auto runB = [&](int wpc) {

@@ -13,9 +13,11 @@ namespace zc {
 // the rolling hash of any byte range is a short Horner fold over spans.
 constexpr int ZC_SPAN = 1024;                                // digest granularity
 constexpr int ZC_TPB = 256;                                  // 4 waves
-// zc_scan: 512-lane persistent workgroups, lane span 4 KiB (2 MiB tiles),
-// per-wave LDS rings of ZC_RING slots of 128-byte rounds.  (The *_CFG macros
-// exist for the geometry sweeps of tools/ubench/scan_ablate.hip.)
+// zc_scan: lane span 4 KiB, a wave's 64 spans a 256 KiB wave-tile, 2 MiB
+// tiles of ZC_SCAN_TPB / 64 wave-tiles (the unit of launch_scan_tiles); each
+// wave stages 128-byte rounds through its own one-slot LDS ring, ZC_SCAN_WAVES
+// waves per persistent workgroup.  (The *_CFG macros exist for the geometry
+// sweeps of tools/ubench/scan_ablate.hip.)
 #ifndef ZC_SCAN_TPB_CFG
 #define ZC_SCAN_TPB_CFG 512
 #endif
@@ -32,7 +34,7 @@ constexpr int ZC_SCAN_TPB = ZC_SCAN_TPB_CFG;
 constexpr int ZC_LSPAN = ZC_LSPAN_CFG;
 constexpr uint64_t ZC_STILE = (uint64_t)ZC_LSPAN * ZC_SCAN_TPB;
 constexpr int ZC_ROUND = ZC_ROUND_CFG;
-constexpr int ZC_RING = 2;
+constexpr int ZC_SCAN_WAVES = 4;
 constexpr int ZC_WLIST = ZC_WLIST_CFG;                       // per-wave LDS list of pieces with anchors
 static_assert(ZC_LSPAN % ZC_SPAN == 0 && ZC_LSPAN / ZC_SPAN % 2 == 0 && ZC_LSPAN <= 4096, "lane span");
 static_assert(ZC_ROUND >= 64 && ZC_ROUND <= 256 && ZC_SPAN % ZC_ROUND == 0, "round");

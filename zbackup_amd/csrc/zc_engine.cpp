@@ -427,11 +427,14 @@ struct zc_ctx {
   std::vector<std::pair<uint64_t, uint64_t>> res_spec_hist;
   std::vector<uint64_t> res_ha, res_hidx;
   std::vector<uint8_t> res_ok;
+  std::vector<uint32_t> res_cls, res_cnext, res_ccur, res_ctail;
   // the probe's candidates, read back into pinned memory: a large copy into
   // pageable memory is staged by pinning the caller's pages, and freeing such
   // pages later (the list's destructor) stalled the next call's first
   // submission by 8-28 ms on the GPU box
   HostBuf<Cand> h_cand;
+  HostBuf<uint32_t> h_cls;  // the epoch's content classes (likewise)
+  HostBuf<Run> h_runs;      // the screen's runs (likewise)
   size_t nrec_done = 0;
   size_t rec_head = 0;
   // every entry point holds this: calls on one context from several threads
@@ -1028,15 +1031,19 @@ class Resolver {
   // ccur_[leader] = first member not consumed.  Empty: every ref leads its
   // own class.
   static constexpr uint32_t kNone = 0xFFFFFFFFu;
-  std::vector<uint32_t> cls_, cnext_, ccur_;
+  std::vector<uint32_t>& cls_ = c_.res_cls;
+  std::vector<uint32_t>& cnext_ = c_.res_cnext;
+  std::vector<uint32_t>& ccur_ = c_.res_ccur;
 
   void load_classes() {
-    cls_.resize(nref_);
-    d2h(c_, cls_.data(), c_.c_cls.p, nref_);
+    c_.h_cls.ensure(nref_);
+    d2h(c_, c_.h_cls.p, c_.c_cls.p, nref_);
     sync(c_);
+    cls_.assign(c_.h_cls.p, c_.h_cls.p + nref_);
     cnext_.assign(nref_, kNone);
     ccur_.resize(nref_);
-    std::vector<uint32_t> tail(nref_);
+    std::vector<uint32_t>& tail = c_.res_ctail;
+    tail.resize(nref_);
     for (uint32_t r = 0; r < nref_; ++r) {
       ccur_[r] = r;
       tail[r] = r;
@@ -1776,10 +1783,11 @@ class Resolver {
     // zc_fscan's per-tile lists are read only where it ran
     bool old_ran = !staged;
     for (uint32_t c : wcnt) old_ran |= c == ZC_FWT_OVERFLOW;
-    std::vector<Run> raw(nruns);
+    c_.h_runs.ensure(nruns);
+    const Run* const raw = c_.h_runs.p;
     std::vector<uint64_t> toff(old_ran ? ntiles - t_first : 0), woff(wcnt.size());
     std::vector<uint32_t> tcnt(old_ran ? ntiles - t_first : 0);
-    d2h(c_, raw.data(), c_.runs.p, nruns);
+    d2h(c_, c_.h_runs.p, c_.runs.p, nruns);
     if (old_ran) {
       d2h(c_, toff.data(), ftile_off_v + t_first, ntiles - t_first);
       d2h(c_, tcnt.data(), ftile_cnt_v + t_first, ntiles - t_first);

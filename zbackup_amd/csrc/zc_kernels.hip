@@ -661,30 +661,38 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   return kDigests / 2 + __builtin_amdgcn_readfirstlane(nst) + 2;
 }
 
-// The workgroup's rounds form one flat sequence over its tiles (32 per
-// tile).  A round is read from its ring slot into registers first; the slot
-// is then refilled with the round two ahead before the round is hashed, so
-// two rounds (16 KiB per wave) are in flight while a wave computes.  The 32
-// bytes before each half of a lane span (they prime the gear) are two
-// per-lane register loads issued together with the DMA of the half's first
-// round, so half and tile boundaries cost no extra pipeline round.
+// Every wave walks whole wave-tiles (256 KiB, 64 lane spans) on its own:
+// wave-tiles wt0 + g, wt0 + g + G, ... for global wave g of G.  Its rounds form
+// one flat sequence over them (32 per wave-tile).  The ring has ONE slot per
+// wave: a round is read from the slot into registers, the slot is refilled
+// with the next round, then the round is hashed -- one round (8 KiB) in flight
+// per wave while it computes.  That leaves 12 KiB of LDS per wave (slot +
+// anchor list), so a CU holds 12 waves, three per SIMD, where the two-slot
+// ring (16 KiB per wave) fit eight: with a third wave per SIMD the VALU finds
+// a ready wave more often while the others wait for their rounds
+// (tools/ubench/scan_occ.hip, outputs identical: 1.525 vs 1.564 ms per 8 GiB,
+// DESIGN 4.1 experiment 18).  The 32 bytes before each half of a lane span
+// (they prime the gear) are two per-lane register loads issued with the DMA
+// of the half's first round, so half and wave-tile boundaries cost no extra
+// pipeline round.
+constexpr int kScanWaves = ZC_SCAN_WAVES;  // per workgroup (one per SIMD)
+constexpr int kScanWgPerCu = 3;            // workgroups resident per CU
 struct ScanLds {
-  uint8_t ring[ZC_SCAN_TPB / 64][ZC_RING * 64 * ZC_ROUND];
-  uint4 wdata[ZC_SCAN_TPB / 64][ZC_WLIST];
-  uint32_t wlist[ZC_SCAN_TPB / 64][ZC_WLIST * 3];
+  uint8_t ring[kScanWaves][64 * ZC_ROUND];
+  uint4 wdata[kScanWaves][ZC_WLIST];
+  uint32_t wlist[kScanWaves][ZC_WLIST * 3];
 };
+static_assert(kScanWgPerCu * sizeof(ScanLds) <= 160 * 1024, "three scan workgroups per CU");
 __device__ __forceinline__ void scan_body(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t wt0, uint64_t nwt, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L) {
-  auto& ring = L.ring;
-  auto& wlist = L.wlist;
-  auto& wdata = L.wdata;
-  constexpr uint32_t kRpt = kRounds;  // rounds per tile
+  constexpr uint32_t kRpt = kRounds;  // rounds per wave-tile
+  constexpr uint32_t kWpt = ZC_SCAN_TPB / 64;  // wave-tiles per 2 MiB tile
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t grid = gridDim.x;
-  uint8_t* myring = ring[wave];
-  WaveList wl{wlist[wave], wdata[wave], 0};
-  const uint32_t ntk = ntiles > blockIdx.x ? (uint32_t)((ntiles - 1 - blockIdx.x) / grid + 1) : 0;
+  const uint32_t gw = blockIdx.x * kScanWaves + wave, nw = gridDim.x * kScanWaves;
+  uint8_t* myring = L.ring[wave];
+  WaveList wl{L.wlist[wave], L.wdata[wave], 0};
+  const uint32_t ntk = nwt > gw ? (uint32_t)((nwt - 1 - gw) / nw + 1) : 0;
   const uint32_t nR = ntk * kRpt;
   // this lane's share of DMA instruction j: row j * (1024 / ZC_ROUND) + lane /
   // kPieces of the wave, the source piece that lands at position lane % kPieces
@@ -699,18 +707,17 @@ __device__ __forceinline__ void scan_body(
   v4u32 warm[2] = {};                       // the 32 bytes before the next half span
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kRpt, r = Rx - k * kRpt;
-    const uint64_t tile = tile0 + blockIdx.x + (uint64_t)k * grid;
-    stage_round<kScanDmaAux>(data, myring, wave, lane_off, tile, (int)r, Rx & 1);
+    const uint64_t wt = wt0 + gw + (uint64_t)k * nw;
+    stage_round<kScanDmaAux>(data, myring, (uint32_t)(wt % kWpt), lane_off, wt / kWpt, (int)r, 0u);
     if (r % kHalfRounds == 0) {
       // span 0 of the stream has no bytes before it: it reads itself (unused)
-      const uint64_t at = tile * ZC_STILE + (uint64_t)tid * ZC_LSPAN + (uint64_t)(r ^ hs) * ZC_ROUND;
+      const uint64_t at = (wt << ZC_WT_SHIFT) + (uint64_t)lane * ZC_LSPAN + (uint64_t)(r ^ hs) * ZC_ROUND;
       const uint8_t* src = at >= 32 ? data + at - 32 : data + at;
       warm[0] = global_read16(src);
       warm[1] = global_read16(src + 16);
     }
   };
   if (nR > 0) issue(0);
-  if (nR > 1) issue(1);
   ScanLane s{0, 0, 0};
   uint64_t bk[kDigests];
 #pragma unroll
@@ -725,18 +732,14 @@ __device__ __forceinline__ void scan_body(
     const uint32_t k = R / kRpt;
     const int r = (int)(R - k * kRpt);
     // round R (and, for a half's first round, its warm-up loads) has landed
-    // once only what was issued after it is outstanding: round R + 1's DMA,
-    // plus the next half's warm-up loads before a half's first round, plus
-    // the tile end's stores before round 0
-    if (R + 1 >= nR) wait_vmcnt<0>();
-    else if ((r + 1) % kHalfRounds == 0) wait_vmcnt<kDmaRound + 2>();
-    else if (r == 0) wait_vmcnt_dyn(kDmaRound + tail_stores);
-    else wait_vmcnt<kDmaRound>();
-    const uint8_t* row = myring + (R & 1) * (64 * ZC_ROUND);
+    // once only what was issued after it is outstanding: nothing, or before a
+    // wave-tile's first round the last tile end's stores
+    if (r == 0) wait_vmcnt_dyn(tail_stores);
+    else wait_vmcnt<0>();
     const uint32_t pr = (uint32_t)r ^ hs;  // the physical round in the lane span
     if (r == 0) {
-      // a new tile
-      span0 = (tile0 + blockIdx.x + (uint64_t)k * grid) * ZC_STILE + (uint64_t)tid * ZC_LSPAN;
+      // a new wave-tile
+      span0 = ((wt0 + gw + (uint64_t)k * nw) << ZC_WT_SHIFT) + (uint64_t)lane * ZC_LSPAN;
       s = ScanLane{0, 0, 0};
       wl.n = 0;
       last = kNoEntry;
@@ -755,21 +758,18 @@ __device__ __forceinline__ void scan_body(
           for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
     }
-    static_assert(kPieces == 8, "the round is read in two halves of four pieces");
+    static_assert(kPieces == 8, "the round is read as eight pieces");
     v4u32 va[4], vb[4];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) va[p] = lds_read16(row + lane * ZC_ROUND + ((p ^ sw) << 4));
+    for (int p = 0; p < 4; ++p) va[p] = lds_read16(myring + lane * ZC_ROUND + ((p ^ sw) << 4));
 #pragma unroll
-    for (int p = 0; p < 4; ++p) vb[p] = lds_read16(row + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
-    // the first four pieces are hashed while the last four are still in flight
-    wait_lgkmcnt<4>();
+    for (int p = 0; p < 4; ++p) vb[p] = lds_read16(myring + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
+    wait_lgkmcnt<0>();  // the slot is read out: refill it with the next round
     ties(va);
-    const bool tile_end = r == kRounds - 1;
+    ties(vb);
+    if (R + 1 < nR) issue(R + 1);
 #pragma unroll
     for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
-    wait_lgkmcnt<0>();  // the slot is free
-    ties(vb);
-    if (R + 2 < nR) issue(R + 2);
 #pragma unroll
     for (int p = 0; p < 4; ++p)
       scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
@@ -780,7 +780,8 @@ __device__ __forceinline__ void scan_body(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (tile_end) tail_stores = scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
+    if (r == kRounds - 1)
+      tail_stores = scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
   }
   if (lane == 0) {
     if (acc_pool) atomicAdd(&counters[CNT_POOL], (unsigned long long)acc_pool);
@@ -788,11 +789,13 @@ __device__ __forceinline__ void scan_body(
   }
 }
 
-__global__ void __launch_bounds__(ZC_SCAN_TPB, 1) zc_scan_kernel(
-    const uint8_t* __restrict__ data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t lo_thr,
+// (__launch_bounds__' second argument: at least three waves per SIMD, i.e. at
+// most 168 VGPRs)
+__global__ void __launch_bounds__(64 * kScanWaves, kScanWgPerCu) zc_scan_kernel(
+    const uint8_t* __restrict__ data, uint64_t n, uint64_t wt0, uint64_t nwt, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
   __shared__ ScanLds lds;
-  scan_body(data, n, tile0, ntiles, lo_thr, blk, po, counters, lds);
+  scan_body(data, n, wt0, nwt, lo_thr, blk, po, counters, lds);
 }
 // the stream's last, partial tile: one 256-thread block per wave-tile, a
 // 1 KiB sub-span per thread (block digests and anchors)
@@ -2620,9 +2623,12 @@ static int cu_count() {
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
                              uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
   if (!ntiles) return hipSuccess;
-  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)cu_count());
-  hipLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(ZC_SCAN_TPB), 0, s, data, n, tile0, ntiles,
-                     anchor_lo, blk, po, counters);
+  // the tiles' wave-tiles, a wave each at a time, three workgroups per CU
+  const uint64_t wt0 = tile0 * (ZC_SCAN_TPB / 64), nwt = ntiles * (ZC_SCAN_TPB / 64);
+  const unsigned grid = (unsigned)std::min<uint64_t>((nwt + kScanWaves - 1) / kScanWaves,
+                                                     (uint64_t)cu_count() * kScanWgPerCu);
+  hipLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(64 * kScanWaves), 0, s, data, n, wt0, nwt, anchor_lo, blk,
+                     po, counters);
   return hipGetLastError();
 }
 
