@@ -106,16 +106,18 @@ occ_scan_kernel(const uint8_t* __restrict__ data, uint64_t n, uint64_t nwt, int3
     v4u32 va[4], vb[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) va[p] = lds_read16(row + lane * ZC_ROUND + ((p ^ sw) << 4));
+    if constexpr (kPieces == 8) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) vb[p] = lds_read16(row + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
+      for (int p = 0; p < 4; ++p) vb[p] = lds_read16(row + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
+    }
     if constexpr (RING == 1) {
       wait_lgkmcnt<0>();  // the slot is read out: refill it with the next round
       ties(va);
-      ties(vb);
+      if constexpr (kPieces == 8) ties(vb);
       if (R + 1 < nR) issue(R + 1);
 #pragma unroll
       for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
-    } else {
+    } else if constexpr (kPieces == 8) {
       wait_lgkmcnt<4>();
       ties(va);
 #pragma unroll
@@ -123,9 +125,17 @@ occ_scan_kernel(const uint8_t* __restrict__ data, uint64_t n, uint64_t nwt, int3
       wait_lgkmcnt<0>();
       ties(vb);
       if (R + 2 < nR) issue(R + 2);
-    }
+    } else {
+      wait_lgkmcnt<0>();
+      ties(va);
+      if (R + 2 < nR) issue(R + 2);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
+      for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
+    }
+    if constexpr (kPieces == 8) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
+    }
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const uint32_t q = pr / (ZC_SPAN / ZC_ROUND);
@@ -171,13 +181,16 @@ int main(int argc, char** argv) {
   const PoolOut po{dbase, dcnt, prel, pg, wcap, 0};
   struct V { const char* name; OccK k; int tpb; int wg_per_cu; std::vector<float> t; uint64_t sig; unsigned long long pool; };
   std::vector<V> vs = {
-    {"product zc_scan_kernel", nullptr, ZC_SCAN_TPB, 1, {}, 0, 0},
-    {"per-wave tiles, 8 waves x1, ring 2, wpe1", occ_scan_kernel<8, 2, 1>, 512, 1, {}, 0, 0},
+    {"product zc_scan_kernel", nullptr, 0, 0, {}, 0, 0},
+#if ZC_ROUND_CFG == 64
+    {"per-wave tiles, 4 waves x4, ring 1, wpe4", occ_scan_kernel<4, 1, 4>, 256, 4, {}, 0, 0},
+    {"per-wave tiles, 4 waves x3, ring 2, wpe3", occ_scan_kernel<4, 2, 3>, 256, 3, {}, 0, 0},
     {"per-wave tiles, 4 waves x3, ring 1, wpe3", occ_scan_kernel<4, 1, 3>, 256, 3, {}, 0, 0},
-    {"product zc_scan_kernel (again)", nullptr, ZC_SCAN_TPB, 1, {}, 0, 0},
+    {"per-wave tiles, 4 waves x4, ring 1, wpe4 (again)", occ_scan_kernel<4, 1, 4>, 256, 4, {}, 0, 0},
+#else
+    {"per-wave tiles, 4 waves x3, ring 1, wpe3", occ_scan_kernel<4, 1, 3>, 256, 3, {}, 0, 0},
     {"per-wave tiles, 2 waves x6, ring 1, wpe3", occ_scan_kernel<2, 1, 3>, 128, 6, {}, 0, 0},
-    {"per-wave tiles, 8 waves x1, ring 2 (again)", occ_scan_kernel<8, 2, 1>, 512, 1, {}, 0, 0},
-    {"per-wave tiles, 4 waves x3, ring 1 (again)", occ_scan_kernel<4, 1, 3>, 256, 3, {}, 0, 0},
+#endif
   };
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   std::vector<uint32_t> h32(n / ZC_SPAN * 2), hc(nwt);

@@ -961,6 +961,11 @@ class Resolver {
   uint64_t lim_ = 0;      // probes below lim_ are resolved by this call
   const uint32_t W_;
   const bool indexable_;
+  // x / W and x % W without a 64-bit division when W is a power of two (the
+  // per-candidate loops run 100 K+ times per stream)
+  const int wsh_ = (W_ & (W_ - 1)) == 0 ? __builtin_ctz(W_) : -1;
+  uint64_t wdiv(uint64_t x) const { return wsh_ >= 0 ? x >> wsh_ : x / W_; }
+  uint64_t wmod(uint64_t x) const { return wsh_ >= 0 ? x & (W_ - 1) : x % W_; }
   uint64_t npool_ = 0;
   const int32_t anchor_lo_ = anchor_lo_for(W_);
   const uint32_t wcap_ = wave_tile_cap(W_);
@@ -1454,8 +1459,8 @@ class Resolver {
         hidx.push_back(i);
         continue;
       }
-      if (!cls_.empty() && ws >= r_e_ && (ws - r_e_) % W_ == 0 && (ws - r_e_) / W_ < nref_ - nconf_) {
-        const uint32_t r = nconf_ + (uint32_t)((ws - r_e_) / W_);
+      if (!cls_.empty() && ws >= r_e_ && wmod(ws - r_e_) == 0 && wdiv(ws - r_e_) < nref_ - nconf_) {
+        const uint32_t r = nconf_ + (uint32_t)wdiv(ws - r_e_);
         if (cls_[r] == hc[i].ref) continue;
       }
       wa.push_back(ws);
@@ -1482,7 +1487,7 @@ class Resolver {
             // speculation), so the walk need not wait for the grid SHA-1
             const uint64_t i = hidx[j];
             hcands_.push_back({hc[i].p, hc[i].ref});
-            spec_hist_.push_back({ha[j] / W_, hc[i].ref});
+            spec_hist_.push_back({wdiv(ha[j]), hc[i].ref});
             continue;
           }
           if (const uint8_t* g = grid_sha_of(ha[j])) {
@@ -2368,12 +2373,12 @@ class Resolver {
   }
   // window [ws, ws + W) is a grid chunk whose SHA-1 the side stream computes
   bool grid_sha_pending(uint64_t ws) const {
-    return pre_sha_n_ && ws % W_ == 0 && ws / W_ < pre_sha_n_ && ws + W_ <= n_;
+    return pre_sha_n_ && wmod(ws) == 0 && wdiv(ws) < pre_sha_n_ && ws + W_ <= n_;
   }
   // grid chunk q's SHA-1 when window [ws, ws + W) is that chunk, else null
   const uint8_t* grid_sha_of(uint64_t ws) {
-    if (!pre_sha_n_ || ws % W_) return nullptr;
-    const uint64_t q = ws / W_;
+    if (!pre_sha_n_ || wmod(ws)) return nullptr;
+    const uint64_t q = wdiv(ws);
     if (q >= pre_sha_n_ || ws + W_ > n_) return nullptr;
     return grid_sha() + 20 * q;
   }

@@ -676,13 +676,16 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
 // of the half's first round, so half and wave-tile boundaries cost no extra
 // pipeline round.
 constexpr int kScanWaves = ZC_SCAN_WAVES;  // per workgroup (one per SIMD)
-constexpr int kScanWgPerCu = 3;            // workgroups resident per CU
+#ifndef ZC_SCAN_WG_PER_CU_CFG
+#define ZC_SCAN_WG_PER_CU_CFG 3
+#endif
+constexpr int kScanWgPerCu = ZC_SCAN_WG_PER_CU_CFG;  // workgroups resident per CU
 struct ScanLds {
   uint8_t ring[kScanWaves][64 * ZC_ROUND];
   uint4 wdata[kScanWaves][ZC_WLIST];
   uint32_t wlist[kScanWaves][ZC_WLIST * 3];
 };
-static_assert(kScanWgPerCu * sizeof(ScanLds) <= 160 * 1024, "three scan workgroups per CU");
+static_assert(kScanWgPerCu * sizeof(ScanLds) <= 160 * 1024, "the scan workgroups of a CU fit its LDS");
 __device__ __forceinline__ void scan_body(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t wt0, uint64_t nwt, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L) {
@@ -758,21 +761,25 @@ __device__ __forceinline__ void scan_body(
           for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
       }
     }
-    static_assert(kPieces == 8, "the round is read as eight pieces");
+    static_assert(kPieces == 8 || kPieces == 4, "the round is read as four or eight pieces");
     v4u32 va[4], vb[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) va[p] = lds_read16(myring + lane * ZC_ROUND + ((p ^ sw) << 4));
+    if constexpr (kPieces == 8) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) vb[p] = lds_read16(myring + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
+      for (int p = 0; p < 4; ++p) vb[p] = lds_read16(myring + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
+    }
     wait_lgkmcnt<0>();  // the slot is read out: refill it with the next round
     ties(va);
-    ties(vb);
+    if constexpr (kPieces == 8) ties(vb);
     if (R + 1 < nR) issue(R + 1);
 #pragma unroll
     for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
+    if constexpr (kPieces == 8) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
-      scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
+      for (int p = 0; p < 4; ++p)
+        scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
+    }
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const uint32_t q = pr / (ZC_SPAN / ZC_ROUND);  // per lane: the halves are rotated
