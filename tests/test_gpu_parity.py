@@ -174,21 +174,22 @@ def test_long_grid_runs_vs_oracle(torch_cuda, spec):
 
 def _dense_anchor_pattern(W, period=16):
     """A `period`-byte pattern whose periodic extension has an anchor in every
-    period at chunk size W (the gear of zc_device.h: sum b[q-j] 2^j mod 2^32 >=
-    anchor_lo), so wave-tiles overflow their anchor-pool share."""
+    period at chunk size W (the anchor state of zc_device.h: st(q) = sum_{j<16}
+    b[q-2j] 2^j mod 2^16, an anchor where (int16)st(q) >= anchor_lo), so
+    wave-tiles overflow their anchor-pool share."""
     rate = 16
     while rate < 4096 and rate * 2 <= W // 16:
         rate *= 2
-    lo = 0x80000000 - (1 << 32) // rate
+    lo = 0x8000 - 0x10000 // rate
     rng = np.random.default_rng(77)
     for _ in range(100000):
         pat = rng.integers(0, 256, period, dtype=np.uint8)
         ext = np.tile(pat, 64 // period + 2)
         for q in range(32, 32 + period):
-            g = 0
-            for j in range(32):
-                g = (g + (int(ext[q - j]) << j)) & 0xFFFFFFFF
-            if lo <= g < 0x80000000:
+            st = 0
+            for j in range(16):
+                st = (st + (int(ext[q - 2 * j]) << j)) & 0xFFFF
+            if lo <= st < 0x8000:
                 return pat
     raise AssertionError("no pattern found")
 

@@ -113,7 +113,7 @@ def test_bloom_screen_odd_w_vs_oracle(torch_cuda, W, nrand):
 def _headed_blocks(nblk, W, seed):
     """nblk W-byte blocks, each 32 seeded random bytes then zeros: all distinct,
     none with an anchor (a chunk's first anchor sits at offset >= 63, where
-    the 32-byte gear window sees only zeros)."""
+    the anchor test's 31-byte window sees only zeros)."""
     rng = np.random.default_rng(seed)
     b = np.zeros((nblk, W), dtype=np.uint8)
     b[:, :32] = rng.integers(0, 256, (nblk, 32), dtype=np.uint8)

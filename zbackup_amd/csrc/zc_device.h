@@ -58,14 +58,18 @@ constexpr uint64_t ZC_FWT = 64ull * ZC_FLSPAN;
 static_assert(ZC_FWT % ZC_TILE == 0, "screen wave-tiles cover whole zc_fscan tiles");
 constexpr uint32_t ZC_FWT_OVERFLOW = 0xFFFFFFFFu;            // wave-tile left for zc_fscan
 
-// Content anchors.  gear(q) = sum_{j<32} b[q-j] * 2^j (mod 2^32); q is an
-// anchor iff (int32)gear(q) >= anchor_lo, i.e. gear in [anchor_lo, 0x7FFFFFFF]:
-// 1 position in rate_inv for random bytes (rate_inv = 2^32 / (2^31 - anchor_lo),
-// chosen per stream from W so a W-byte chunk holds ~16 anchors), never inside a
-// run of one repeated byte (gear 0 or -c).  Every position is tested, so a
-// window holds the anchors of its content at any alignment.  A chunk's anchor
-// is its first one at offset >= ZC_ANCHOR_MIN_OFF; the table key is the gear
-// value, confirmed by a 64-bit fingerprint of the 8 bytes ending at the anchor.
+// Content anchors.  st(q) = sum_{j<16} b[q-2j] * 2^j (mod 2^16), a 16-bit
+// gear over the bytes of q's parity (window [q-30, q]); q is an anchor iff
+// (int16)st(q) >= anchor_lo, i.e. st in [anchor_lo, 0x7FFF]: 1 position in
+// rate_inv for random bytes (rate_inv = 2^16 / (2^15 - anchor_lo), chosen per
+// stream from W so a W-byte chunk holds ~16 anchors), never inside a run of
+// one repeated byte (st 0 or -c).  Every position is tested, so a window holds
+// the anchors of its content at any alignment.  A chunk's anchor is its first
+// one at offset >= ZC_ANCHOR_MIN_OFF; the table key is {st(q-1), st(q)} (the
+// 32 bytes ending at q; its top 12 bits are fixed by the anchor test, its low
+// 20 free), confirmed by a 64-bit fingerprint of the 8 bytes ending at q.
+// (Two 16-bit streams instead of one 32-bit gear: the scan advances both with
+// one v_pk_mad_u16)
 constexpr uint32_t ZC_ANCHOR_MIN_OFF = 63;
 constexpr uint32_t ZC_NO_ANCHOR = 0xFFFFFFFFu;
 
@@ -74,9 +78,7 @@ inline uint32_t anchor_rate_inv(uint32_t W) {
   while (rate_inv < 4096 && rate_inv * 2 <= W / 16) rate_inv *= 2;
   return rate_inv;
 }
-inline int32_t anchor_lo_for(uint32_t W) {
-  return (int32_t)(0x80000000u - (uint32_t)(0x100000000ull / anchor_rate_inv(W)));
-}
+inline int32_t anchor_lo_for(uint32_t W) { return (int32_t)(0x8000u - 0x10000u / anchor_rate_inv(W)); }
 
 // Anchors of the stream, per wave-tile t: cnt[t] anchors, sorted by position,
 // at index base[t] of the pool (rel = position - (t << ZC_WT_SHIFT), g = gear

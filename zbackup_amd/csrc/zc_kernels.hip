@@ -206,11 +206,46 @@ __device__ __forceinline__ uint32_t load4_any(const uint8_t* base, uint64_t addr
 // and moved to the per-span global slots once per tile, so no global store is
 // outstanding while the ring is being waited on.
 struct ScanLane {
-  uint32_t glo;       // gear hash
+  uint32_t glo;       // anchor state {st(q - 1), st(q)} after position q (zc_device.h)
   uint32_t hlo, hhi;  // 64-bit Rabin-Karp accumulator of the current 1 KiB span
 };
 
-__device__ __forceinline__ void gear_step(uint32_t b, ScanLane& s) { s.glo = (s.glo << 1) + b; }
+// One byte of the anchor state: st(q + 1) = 2 st(q - 1) + b[q + 1] (mod 2^16)
+// joins as the high half, st(q) moves down.  The scalar form (tail, rescan).
+__device__ __forceinline__ void gear_step(uint32_t b, ScanLane& s) {
+  s.glo = (s.glo >> 16) | (((s.glo << 1) + b) << 16);
+}
+
+// The packed form: the two halves of the state are the even- and odd-position
+// streams, so v_pk_mad_u16 advances both by one byte each.  A dword at an even
+// position 4t: {b0, b1} and {b2, b3} as u16 pairs (one v_perm each), two
+// steps; the state after the first is {st(4t), st(4t + 1)}, after the second
+// {st(4t + 2), st(4t + 3)}.  `two` is 0x00020002 (an SGPR operand keeps the
+// compiler from splitting the multiply into a shift and an add).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_step(uint32_t S, uint32_t P, uint32_t two) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, S) * __builtin_bit_cast(u16x2, two) +
+                                          __builtin_bit_cast(u16x2, P));
+}
+__device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, a),
+                                                                __builtin_bit_cast(i16x2, b)));
+}
+__device__ __forceinline__ uint32_t bytes01(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0C010C00u); }
+__device__ __forceinline__ uint32_t bytes23(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0C030C02u); }
+// the larger signed half of a packed pair
+__device__ __forceinline__ int32_t hmax16(uint32_t m) { return max((int32_t)(int16_t)m, (int32_t)m >> 16); }
+__device__ __forceinline__ uint32_t pk_two() {
+  uint32_t t;
+  asm volatile("s_mov_b32 %0, 0x20002" : "=s"(t));
+  return t;
+}
+// The anchor key at each position of a dword, from the state before it (S)
+// and after its two steps (S1, S2): {st(q - 1), st(q)} for q = 4t .. 4t + 3
+__device__ __forceinline__ uint32_t dword_key(uint32_t S, uint32_t S1, uint32_t S2, uint32_t k) {
+  return k == 0 ? __builtin_amdgcn_alignbit(S1, S, 16) : k == 1 ? S1 : k == 2 ? __builtin_amdgcn_alignbit(S2, S1, 16) : S2;
+}
 
 __device__ __forceinline__ void digest_step(uint32_t b, ScanLane& s) {
   // acc*257 + b  (mod 2^64)
@@ -226,8 +261,8 @@ __device__ __forceinline__ void digest_step(uint32_t b, ScanLane& s) {
 // (chunks and stream windows) use this one.
 __device__ __forceinline__ uint32_t load4_any(const uint8_t* base, uint64_t addr);
 __device__ uint64_t anchor_fp(const uint8_t* __restrict__ data, uint64_t q) {
-  // the 8 bytes ending at q (the gear value adds the 32 before; an anchor's
-  // gear has only ~20 free bits, these 64 make a false match rare)
+  // the 8 bytes ending at q (the anchor key adds the 32 before; a key has
+  // only ~20 free bits, these 64 make a false match rare)
   return ((uint64_t)load4_any(data, q - 3) << 32) | load4_any(data, q - 7);
 }
 
@@ -248,46 +283,41 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// One 16-byte piece of the scan (four dwords).  Gear: position k of a dword is
-// g_k = (g << (k+1)) + sum_{j<=k} b_j 2^(k-j), the byte-weighted sums coming
-// from v_dot4_u32_u8, so the four positions are independent of each other.
-// Digest: two bytes per step, acc*257^2 + (257 b_0 + b_1) (v_perm + SDWA
-// add for the pair, two v_mad_u64_u32 for the 64-bit multiply-add).  Anchor
-// test: the max of the piece's sixteen gears (two v_max3 per dword), one
-// compare and one ballot per piece.  The recording block is wave-uniform (the
+// One 16-byte piece of the scan (four dwords).  Anchor state: two v_perm give
+// a dword's byte pairs {b0, b1}, {b2, b3}; two v_pk_mad_u16 advance the even
+// and the odd stream (pk_step).  Digest: two bytes per step, acc*257^2 +
+// (257 b_0 + b_1), the addend a v_dot2_u32_u16 of the same byte pair, the
+// 64-bit multiply-add a v_mul_lo_u32 + v_mad_u64_u32.  Anchor test: a
+// v_pk_max_i16 chain over the piece's sixteen states (two per dword), one
+// compare and one ballot per piece: 12 VALU per dword where the 32-bit gear
+// took 16.5.  The recording block is wave-uniform (the
 // list count stays scalar) and entered for ~22 % of pieces at the 1/4096
-// anchor rate: each lane with a hit appends the piece (its bytes, the gear
+// anchor rate: each lane with a hit appends the piece (its bytes, the state
 // before it and a link to the lane's previous entry) to the wave's LDS list,
 // and the tile end re-derives the exact anchors from those 16 bytes.
 // (Anchors tested at dword ends alone -- a quarter of the positions -- save
 // 6 % of the kernel, but windows at other alignments then need every chunk's
 // anchors in four residues, whose search costs more than that: DESIGN 4.1,
 // experiment 16.)
-__device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr, ScanLane& s, WaveList& wl,
-                                           uint32_t& last) {
+__device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr, uint32_t two, ScanLane& s,
+                                           WaveList& wl, uint32_t& last) {
   const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-  const uint32_t g0 = s.glo;  // gear before the piece
-  uint32_t g[4][4];
-  int32_t mx[4];
+  const uint32_t g0 = s.glo;  // anchor state before the piece
+  uint32_t m = 0;
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t x = xs[d];
-    const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
-                            __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
-                            __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) g[d][k] = (s.glo << (k + 1)) + dd[k];
-    s.glo = g[d][3];
-    // one max3 chain over the piece's 16 gears (8 v_max3_i32 per piece)
-    mx[d] = d == 0 ? max(max((int32_t)g[0][0], (int32_t)g[0][1]), (int32_t)g[0][2])
-                   : max(max(mx[d - 1], (int32_t)g[d - 1][3]), (int32_t)g[d][0]);
-    if (d > 0) mx[d] = max(max(mx[d], (int32_t)g[d][1]), (int32_t)g[d][2]);
-    // two bytes per Horner step: acc*257^2 + (257 b_0 + b_1).  One v_perm
-    // swaps the bytes of each half (b_1 | b_0 << 8), an SDWA add adds b_0;
-    // acc*66049 + t is a v_mad_u64_u32 on the low word and one on the
-    // high word: 9 lane-ops per dword instead of 12
-    const uint32_t sp = __builtin_amdgcn_perm(0u, x, 0x02030001u);
-    const uint32_t t[2] = {(sp & 0xFFFFu) + (x & 0xFFu), (sp >> 16) + ((x >> 16) & 0xFFu)};
+    // the byte pairs feed both the anchor state and the digest
+    const uint32_t p01 = bytes01(x), p23 = bytes23(x);
+    const uint32_t S1 = pk_step(s.glo, p01, two), S2 = pk_step(S1, p23, two);
+    s.glo = S2;
+    // one v_pk_max_i16 chain over the piece's 16 states (st(q) of every q)
+    m = d == 0 ? pk_max16(S1, S2) : pk_max16(pk_max16(m, S1), S2);
+    // two bytes per Horner step: acc*257^2 + (257 b_0 + b_1), the addend one
+    // v_dot2_u32_u16 of a byte pair; acc*66049 + t is a v_mad_u64_u32 on the
+    // low word and a v_mul_lo_u32 on the high one
+    const uint32_t t[2] = {__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p01), (u16x2){257, 1}, 0u, false),
+                           __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, p23), (u16x2){257, 1}, 0u, false)};
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       // acc*66049 + t = lo*66049 + {t, hi*66049}: a v_mul_lo_u32 for the
@@ -298,11 +328,11 @@ __device__ __forceinline__ void scan_piece(uint4 v, uint32_t rel, int32_t lo_thr
       s.hlo = (uint32_t)R;
     }
   }
-  const int32_t m = max(mx[3], (int32_t)g[3][3]);
-  const uint64_t any = __ballot(m >= lo_thr);
+  const bool hit = hmax16(m) >= lo_thr;
+  const uint64_t any = __ballot(hit);
   if (__builtin_expect(any != 0, 0)) {
     const uint32_t idx = wl.n + lane_prefix(any);
-    if (m >= lo_thr && idx < ZC_WLIST) {
+    if (hit && idx < ZC_WLIST) {
       wl.e[3 * idx] = ((rel >> 4) << 8) | last | (__lane_id() << 16);
       wl.e[3 * idx + 1] = g0;
       wl.x[idx] = v;
@@ -356,7 +386,7 @@ __device__ uint64_t subspan_pass(const uint8_t* __restrict__ data, uint64_t n, u
             const uint32_t b = (xs[d] >> (8 * j)) & 0xFFu;
             gear_step(b, s);
             digest_step(b, s);
-            if ((int32_t)s.glo >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) emit(p, s.glo);
+            if (((int32_t)s.glo >> 16) >= lo_thr && p >= ZC_ANCHOR_MIN_OFF) emit(p, s.glo);
           }
         }
     }
@@ -534,16 +564,17 @@ __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, 
   h.xs[1] = v.y;
   h.xs[2] = v.z;
   h.xs[3] = v.w;
-  uint32_t g = h.g0, mask = 0;
+  const uint32_t two = 0x00020002u;
+  uint32_t S = h.g0, mask = 0;
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const uint32_t x = h.xs[d];
-    const uint32_t dd[4] = {x & 0xFFu, __builtin_amdgcn_udot4(x, 0x00000102u, 0u, false),
-                            __builtin_amdgcn_udot4(x, 0x00010204u, 0u, false),
-                            __builtin_amdgcn_udot4(x, 0x01020408u, 0u, false)};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) mask |= ((int32_t)((g << (k + 1)) + dd[k]) >= lo_thr) ? 1u << (4 * d + k) : 0u;
-    g = (g << 4) + dd[3];
+    const uint32_t S1 = pk_step(S, bytes01(h.xs[d]), two), S2 = pk_step(S1, bytes23(h.xs[d]), two);
+    // st(q) of the dword's four positions: the halves of S1, then of S2
+    mask |= ((int32_t)(int16_t)S1 >= lo_thr ? 1u : 0u) << (4 * d);
+    mask |= (((int32_t)S1 >> 16) >= lo_thr ? 1u : 0u) << (4 * d + 1);
+    mask |= ((int32_t)(int16_t)S2 >= lo_thr ? 1u : 0u) << (4 * d + 2);
+    mask |= (((int32_t)S2 >> 16) >= lo_thr ? 1u : 0u) << (4 * d + 3);
+    S = S2;
   }
   if (span0 + h.rel < ZC_ANCHOR_MIN_OFF)  // the stream's first 63 positions are no anchors
     mask &= ~0u << min(ZC_ANCHOR_MIN_OFF - (uint32_t)(span0 + h.rel), 16u);
@@ -627,10 +658,11 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
           xs[1] = v.y;
           xs[2] = v.z;
           xs[3] = v.w;
-          // the gear before each dword of the piece
+          // the anchor state before each dword of the piece
           gd[0] = wl.e[3 * i + 1];
 #pragma unroll
-          for (int d = 0; d < 3; ++d) gd[d + 1] = (gd[d] << 4) + __builtin_amdgcn_udot4(xs[d], 0x01020408u, 0u, false);
+          for (int d = 0; d < 3; ++d)
+            gd[d + 1] = pk_step(pk_step(gd[d], bytes01(xs[d]), 0x00020002u), bytes23(xs[d]), 0x00020002u);
           i += 64;
         }
         if (__ballot(mask != 0) == 0) break;
@@ -638,9 +670,9 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
           const uint32_t t = __builtin_ctz(mask), d = t >> 2, q = t & 3u;
           const uint32_t gdd = d == 0 ? gd[0] : d == 1 ? gd[1] : d == 2 ? gd[2] : gd[3];
           const uint32_t xd = d == 0 ? xs[0] : d == 1 ? xs[1] : d == 2 ? xs[2] : xs[3];
-          // g at position t: the dword's gear shifted q + 1, plus its first q + 1
-          // bytes weighted 2^(q - j)
-          const uint32_t g = (gdd << (q + 1)) + __builtin_amdgcn_udot4(xd, 0x01020408u >> (8 * (3 - q)), 0u, false);
+          // the key at position t: {st(t - 1), st(t)} from the dword's state
+          const uint32_t S1 = pk_step(gdd, bytes01(xd), 0x00020002u), S2 = pk_step(S1, bytes23(xd), 0x00020002u);
+          const uint32_t g = dword_key(gdd, S1, S2, q);
           po.rel[base + w] = sb + t;
           po.g[base + w] = g;
           mask &= mask - 1;
@@ -706,6 +738,7 @@ __device__ __forceinline__ void scan_body(
     lane_off[j] = row * ZC_LSPAN + (row & 1) * kHalfSpan + ((lane % kPieces) ^ row_swizzle(row)) * 16;
   }
   const uint32_t sw = row_swizzle(lane);  // read-side swizzle of this lane's row
+  const uint32_t two = pk_two();          // the packed state's multiplier, in an SGPR
   const uint32_t hs = (lane & 1) * kHalfRounds;  // logical round r is physical round r ^ hs
   v4u32 warm[2] = {};                       // the 32 bytes before the next half span
   auto issue = [&](uint32_t Rx) {
@@ -748,17 +781,16 @@ __device__ __forceinline__ void scan_body(
       last = kNoEntry;
     }
     if (r % kHalfRounds == 0) {
-      // a new half: the warm-up bytes prime the gear (its value depends on the
-      // 32 bytes before only, so this equals the gear rolled on continuously)
+      // a new half: the warm-up bytes prime the anchor state (it depends on
+      // the 32 bytes before only, so this equals the state rolled on
+      // continuously)
       s.glo = 0;
       ties(warm);  // landed: the wait above covers them
       if (span0 + pr * ZC_ROUND >= 64) {
         const uint32_t xs[8] = {warm[0][0], warm[0][1], warm[0][2], warm[0][3],
                                 warm[1][0], warm[1][1], warm[1][2], warm[1][3]};
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) gear_step((xs[j] >> (8 * q)) & 0xFFu, s);
+        for (int j = 0; j < 8; ++j) s.glo = pk_step(pk_step(s.glo, bytes01(xs[j]), two), bytes23(xs[j]), two);
       }
     }
     static_assert(kPieces == 8 || kPieces == 4, "the round is read as four or eight pieces");
@@ -774,11 +806,11 @@ __device__ __forceinline__ void scan_body(
     if constexpr (kPieces == 8) ties(vb);
     if (R + 1 < nR) issue(R + 1);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, s, wl, last);
+    for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, two, s, wl, last);
     if constexpr (kPieces == 8) {
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, s, wl, last);
+        scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, two, s, wl, last);
     }
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
