@@ -1,5 +1,5 @@
 // A/B of scan geometries, interleaved in one process: the product zc_scan_kernel
-// built with different workgroups per CU / anchor-list sizes (scan_variant.hip,
+// built with different workgroups per CU / round sizes / anchor-list sizes (scan_variant.hip,
 // one object per variant, tools/ubench/make_geom_ab.sh), 8 GiB of seeded
 // random bytes.  Span digests compared (identical in every variant); the
 // anchor count is printed (a variant whose list is small overflows wave-tiles,
@@ -14,7 +14,7 @@
 typedef hipError_t (*ScanFn)(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                              uint32_t, unsigned long long*);
 #define DECL(N) extern "C" hipError_t N(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t, unsigned long long*);
-DECL(scan_v_prod) DECL(scan_v_wg4_l64) DECL(scan_v_wg4_l48) DECL(scan_v_wg2)
+DECL(scan_v_prod) DECL(scan_v_r256_wg2) DECL(scan_v_wg2)
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 __global__ void fill(uint8_t* d, uint64_t n) {
@@ -35,8 +35,7 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, n);
   struct V { const char* name; ScanFn f; uint64_t* blk; std::vector<float> t; unsigned long long pool; };
   std::vector<V> vs = {{"3 x 4 waves, list 144 (product)", scan_v_prod, nullptr, {}, 0},
-                       {"4 x 4 waves, list 64", scan_v_wg4_l64, nullptr, {}, 0},
-                       {"4 x 4 waves, list 48", scan_v_wg4_l48, nullptr, {}, 0},
+                       {"2 x 4 waves, 256-byte rounds", scan_v_r256_wg2, nullptr, {}, 0},
                        {"2 x 4 waves, list 144", scan_v_wg2, nullptr, {}, 0}};
   uint32_t *dbase, *dcnt, *prel, *pg; unsigned long long* cnt;
   CK(hipMalloc(&dbase, nwt * 4)); CK(hipMalloc(&dcnt, nwt * 4));

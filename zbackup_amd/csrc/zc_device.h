@@ -278,7 +278,8 @@ struct EpochIndex {
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
-                              hipStream_t s);
+                              hipStream_t s,
+                              hipEvent_t after_meta = nullptr);
 // the SHA-1 pairs of the last launch_epoch_index (counters[CNT_SPAIRS]): key +
 // SHA-1-prefix equality (ChunkIndex::findChunk's test, chunk_index.cc:119-143)
 // decides the class; gsha must be complete (ordered after the SHA-1 kernel),

@@ -1226,8 +1226,12 @@ class Resolver {
       auto tm = Clock::now();
       EpochIndex ix{};
       const bool anchors = !scan_checked_ || npool_ > 0;  // unchecked: assume some
-      uint32_t tbits = 10;  // sized for every ref having an anchor
-      while ((1u << tbits) < 2u * nref_) ++tbits;
+      // sized for every ref having an anchor, at most a quarter full: the
+      // inserts' CAS chains and the probe's walks stay short (at a half,
+      // zc_index_insert took 36 us per 131,072 refs, at a quarter 26, and the
+      // probe 69 -> 59 us; an eighth saves no more than its larger clear costs)
+      uint32_t tbits = 10;
+      while ((1u << tbits) < 4u * nref_) ++tbits;
       if (anchors) {
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         if (nref_) {
@@ -1264,18 +1268,21 @@ class Resolver {
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
                         pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_};
-        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
+        // ev_idx after the chunk metadata: the keys' copy to the host and the
+        // tail digests (copy stream) run beside the rest of the index build
+        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream,
+                               c_.ev_idx));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
         dev_nspec_ = nsref;
         dev_valid_ = true;
       } else {
         HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+        HCK(hipEventRecord(c_.ev_idx, c_.stream));
       }
       // the grid chunks' keys go to the host on the side stream while the
-      // probe runs (the probe is queued first: nothing waits for the host to
-      // set up the side stream)
-      HCK(hipEventRecord(c_.ev_idx, c_.stream));
+      // index build and the probe run (the probe is queued first: nothing
+      // waits for the host to set up the side stream)
       const uint64_t* tab = nref_ && anchors ? c_.tab.p : nullptr;
       // ZC_FLAG_SHA1, speculative (spec_): equal-key grid pairs are joined
       // before the probe (a no-op without pairs; the count is on the device),

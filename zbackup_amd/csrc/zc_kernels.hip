@@ -793,25 +793,23 @@ __device__ __forceinline__ void scan_body(
         for (int j = 0; j < 8; ++j) s.glo = pk_step(pk_step(s.glo, bytes01(xs[j]), two), bytes23(xs[j]), two);
       }
     }
-    static_assert(kPieces == 8 || kPieces == 4, "the round is read as four or eight pieces");
-    v4u32 va[4], vb[4];
+    // the round's pieces, in groups of four (one ties() each)
+    static_assert(kPieces % 4 == 0 && kPieces <= 16, "the round is read as 4, 8 or 16 pieces");
+    constexpr int kGroups = kPieces / 4;
+    v4u32 vg[kGroups][4];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) va[p] = lds_read16(myring + lane * ZC_ROUND + ((p ^ sw) << 4));
-    if constexpr (kPieces == 8) {
+    for (int g = 0; g < kGroups; ++g)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) vb[p] = lds_read16(myring + lane * ZC_ROUND + (((p + 4) ^ sw) << 4));
-    }
+      for (int p = 0; p < 4; ++p) vg[g][p] = lds_read16(myring + lane * ZC_ROUND + (((4 * g + p) ^ sw) << 4));
     wait_lgkmcnt<0>();  // the slot is read out: refill it with the next round
-    ties(va);
-    if constexpr (kPieces == 8) ties(vb);
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) ties(vg[g]);
     if (R + 1 < nR) issue(R + 1);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) scan_piece(to_uint4(va[p]), pr * ZC_ROUND + p * 16, lo_thr, two, s, wl, last);
-    if constexpr (kPieces == 8) {
+    for (int g = 0; g < kGroups; ++g)
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        scan_piece(to_uint4(vb[p]), pr * ZC_ROUND + (p + 4) * 16, lo_thr, two, s, wl, last);
-    }
+        scan_piece(to_uint4(vg[g][p]), pr * ZC_ROUND + (4 * g + p) * 16, lo_thr, two, s, wl, last);
     if ((r + 1) % (ZC_SPAN / ZC_ROUND) == 0) {
       const uint64_t h = ((uint64_t)s.hhi << 32) | s.hlo;
       const uint32_t q = pr / (ZC_SPAN / ZC_ROUND);  // per lane: the halves are rotated
@@ -1108,18 +1106,25 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
     if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
     if (slot.x == gk) {
       const uint32_t ref = slot.y;
-      if (fp == (((uint64_t)slot.w << 32) | slot.z) && cls[ref] == ref) {
-        const uint64_t o = anc_off[ref];
+      // everything indexed by ref in one round of loads (one dependent level
+      // after the slot instead of two)
+      const uint32_t cr = cls[ref], o32 = anc_off[ref];
+      const uint64_t vr = vis[ref];
+      const uint8_t dr = dead[ref];
+      if (fp == (((uint64_t)slot.w << 32) | slot.z) && cr == ref) {
+        const uint64_t o = o32;
         if (pos >= r + o) {
           const uint64_t ws = pos - o, p = ws + W - 1;
           // a window that is a grid chunk of this epoch in ref's class is the
-          // walk's (grid shortcut): no candidate
+          // walk's (grid shortcut): no candidate.  The common case is the grid
+          // chunk's own first anchor (ref = nconf + j, whose class is ref):
+          // known without reading cls[nconf + j]
           bool grid_twin = false;
           if (ws >= eg.r_e && (ws - eg.r_e) % W == 0) {
             const uint64_t j = (ws - eg.r_e) / W;
-            grid_twin = j < eg.nspec && cls[eg.nconf + j] == ref;
+            grid_twin = j < eg.nspec && (eg.nconf + j == ref || cls[eg.nconf + j] == ref);
           }
-          if (p < n && p >= vis[ref] && !dead[ref] && !grid_twin) {
+          if (p < n && p >= vr && !dr && !grid_twin) {
             const unsigned long long c = atomicAdd(&counters[CNT_CAND], 1ull);
             if (c < cand_cap) {
               cand[c].p = p;
@@ -2701,7 +2706,7 @@ hipError_t launch_anchor_rescan(const uint8_t* data, uint64_t n, int32_t anchor_
 
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
-                              hipStream_t s) {
+                              hipStream_t s, hipEvent_t after_meta) {
   const uint32_t nref = nconf + nsref;
   const EpochClear ec{ix.ckeys, nref ? 1u << ix.cbits : 0u, ix.tab,
                       ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters};
@@ -2711,6 +2716,10 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
                      nsref, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
                      ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ec);
+  if (after_meta) {
+    const hipError_t e = hipEventRecord(after_meta, s);
+    if (e != hipSuccess) return e;
+  }
   if (!nref) return hipGetLastError();
   hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
                      ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
