@@ -14,7 +14,7 @@
 typedef hipError_t (*ScanFn)(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                              uint32_t, unsigned long long*);
 #define DECL(N) extern "C" hipError_t N(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t, unsigned long long*);
-DECL(scan_v_prod) DECL(scan_v_r256_wg2) DECL(scan_v_wg2)
+DECL(scan_v_prod) DECL(scan_v_ls2k) DECL(scan_v_ls2k_wg2) DECL(scan_v_wg3)
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 __global__ void fill(uint8_t* d, uint64_t n) {
@@ -29,14 +29,17 @@ __global__ void fill(uint8_t* d, uint64_t n) {
 int main(int argc, char** argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 0) : (8ull << 30);
   const int rounds = argc > 2 ? atoi(argv[2]) : 25;
-  const uint64_t stile = 2ull << 20, ntiles = n / stile, nwt = ntiles * 8, nblk = n / 1024;
+  // sized for the smallest geometry built (2 KiB lane spans: 128 KiB
+  // wave-tiles, 128 pool entries each); each variant launches its own tiles
+  const uint64_t ntiles = n / (2ull << 20), nwt = n / (128ull << 10), nblk = n / 1024;
   const uint32_t wcap = 2u * ((1u << 18) / 4096) + 64u;
   uint8_t* d; CK(hipMalloc(&d, n));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, n);
   struct V { const char* name; ScanFn f; uint64_t* blk; std::vector<float> t; unsigned long long pool; };
-  std::vector<V> vs = {{"3 x 4 waves, list 144 (product)", scan_v_prod, nullptr, {}, 0},
-                       {"2 x 4 waves, 256-byte rounds", scan_v_r256_wg2, nullptr, {}, 0},
-                       {"2 x 4 waves, list 144", scan_v_wg2, nullptr, {}, 0}};
+  std::vector<V> vs = {{"product (2 x 4 waves, list 144)", scan_v_prod, nullptr, {}, 0},
+                       {"3 x 4 waves, 2 KiB lane spans", scan_v_ls2k, nullptr, {}, 0},
+                       {"2 x 4 waves, 2 KiB lane spans", scan_v_ls2k_wg2, nullptr, {}, 0},
+                       {"3 x 4 waves, list 144", scan_v_wg3, nullptr, {}, 0}};
   uint32_t *dbase, *dcnt, *prel, *pg; unsigned long long* cnt;
   CK(hipMalloc(&dbase, nwt * 4)); CK(hipMalloc(&dcnt, nwt * 4));
   CK(hipMalloc(&prel, nwt * wcap * 4)); CK(hipMalloc(&pg, nwt * wcap * 4)); CK(hipMalloc(&cnt, 64));

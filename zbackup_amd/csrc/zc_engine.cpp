@@ -1121,6 +1121,13 @@ class Resolver {
   void scan_finish() {
     meta_from_scan_ = scan_open_;
     if ((c_.flags & ZC_FLAG_TIMING) && scan_open_) HCK(hipEventRecord(c_.ev1, c_.stream));
+    // the side stream's work of the next epoch (tail digests) needs the scan's
+    // span digests only: it waits for this marker, not for one inside the
+    // epoch's batch (a marker between two kernels costs the batch ~7 us)
+    if (scan_open_) {
+      if (!(c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_idx, c_.stream));
+      side_wait_ = (c_.flags & ZC_FLAG_TIMING) ? c_.ev1 : c_.ev_idx;
+    }
     c_.h_scnt.ensure(CNT_LAST);
     d2h(c_, c_.h_scnt.p, c_.counters.p, CNT_LAST);
     scan_checked_ = false;
@@ -1184,6 +1191,7 @@ class Resolver {
   }
   bool scan_checked_ = true;
   bool meta_from_scan_ = false;  // ev1 marks the end of scan launches queued for this batch
+  hipEvent_t side_wait_ = nullptr;  // the copy stream's next work waits for this scan end
 
   // ---------------------------------------------------------------- epoch
   // One epoch = one grid origin r_e.  Device work is queued back to back
@@ -1267,22 +1275,15 @@ class Resolver {
                         c_.c_g.p,     c_.c_fp.p,  c_.c_anc.p,  c_.c_cls.p,
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
-                        pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_};
-        // ev_idx after the chunk metadata: the keys' copy to the host and the
-        // tail digests (copy stream) run beside the rest of the index build
-        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream,
-                               c_.ev_idx));
+                        pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_, nsref ? c_.h_key.p : nullptr};
+        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
         dev_nspec_ = nsref;
         dev_valid_ = true;
       } else {
         HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
-        HCK(hipEventRecord(c_.ev_idx, c_.stream));
       }
-      // the grid chunks' keys go to the host on the side stream while the
-      // index build and the probe run (the probe is queued first: nothing
-      // waits for the host to set up the side stream)
       const uint64_t* tab = nref_ && anchors ? c_.tab.p : nullptr;
       // ZC_FLAG_SHA1, speculative (spec_): equal-key grid pairs are joined
       // before the probe (a no-op without pairs; the count is on the device),
@@ -1294,10 +1295,12 @@ class Resolver {
                          c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
                          c_.stream));
       sha_launch();
-      HCK(hipStreamWaitEvent(c_.copy_stream, c_.ev_idx, 0));
-      if (nsref)
-        HCK(hipMemcpyAsync(c_.h_key.p, c_.c_key.p + nconf_, nsref * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                           c_.copy_stream));
+      // (the grid chunks' keys reach the host from the metadata kernel itself;
+      // the tail digests below need the scan's span digests)
+      if (side_wait_) {
+        HCK(hipStreamWaitEvent(c_.copy_stream, side_wait_, 0));
+        side_wait_ = nullptr;
+      }
       predict_tail();
       // the walk writes this many grid records at once: have the record team
       // spinning by the time the batch is in

@@ -698,18 +698,18 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
 // one flat sequence over them (32 per wave-tile).  The ring has ONE slot per
 // wave: a round is read from the slot into registers, the slot is refilled
 // with the next round, then the round is hashed -- one round (8 KiB) in flight
-// per wave while it computes.  That leaves 12 KiB of LDS per wave (slot +
-// anchor list), so a CU holds 12 waves, three per SIMD, where the two-slot
-// ring (16 KiB per wave) fit eight: with a third wave per SIMD the VALU finds
-// a ready wave more often while the others wait for their rounds
-// (tools/ubench/scan_occ.hip, outputs identical: 1.525 vs 1.564 ms per 8 GiB,
-// DESIGN 4.1 experiment 18).  The 32 bytes before each half of a lane span
-// (they prime the gear) are two per-lane register loads issued with the DMA
-// of the half's first round, so half and wave-tile boundaries cost no extra
-// pipeline round.
+// per wave while it computes; 12 KiB of LDS per wave (slot + anchor list).
+// Two 4-wave workgroups per CU (two waves per SIMD): with the 32-bit gear
+// (16.5 VALU per dword) a third wave per SIMD paid (1.525 vs 1.564 ms per
+// 8 GiB, DESIGN 4.1 experiment 18); with the packed anchor state (12 per
+// dword) two are 1.5 % faster than three (tools/ubench/scan_geom_ab.hip, three
+// interleaved runs, outputs identical; experiment 21).  The 32 bytes before
+// each half of a lane span (they prime the anchor state) are two per-lane
+// register loads issued with the DMA of the half's first round, so half and
+// wave-tile boundaries cost no extra pipeline round.
 constexpr int kScanWaves = ZC_SCAN_WAVES;  // per workgroup (one per SIMD)
 #ifndef ZC_SCAN_WG_PER_CU_CFG
-#define ZC_SCAN_WG_PER_CU_CFG 3
+#define ZC_SCAN_WG_PER_CU_CFG 2
 #endif
 constexpr int kScanWgPerCu = ZC_SCAN_WG_PER_CU_CFG;  // workgroups resident per CU
 struct ScanLds {
@@ -826,8 +826,7 @@ __device__ __forceinline__ void scan_body(
   }
 }
 
-// (__launch_bounds__' second argument: at least three waves per SIMD, i.e. at
-// most 168 VGPRs)
+// (__launch_bounds__' second argument: at least kScanWgPerCu waves per SIMD)
 __global__ void __launch_bounds__(64 * kScanWaves, kScanWgPerCu) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t wt0, uint64_t nwt, int32_t lo_thr,
     uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
@@ -986,7 +985,7 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
                                      uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
                                      uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
-                                     uint32_t* __restrict__ anc_off, EpochClear ec) {
+                                     uint32_t* __restrict__ anc_off, uint64_t* __restrict__ hkey, EpochClear ec) {
   ZC_URGENT();
   const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
@@ -1000,7 +999,11 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   start[i] = c;
   vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
   dead[i] = 0;
-  key[i] = pw + rk_acc(data, blk, c, c + W);
+  const uint64_t k = pw + rk_acc(data, blk, c, c + W);
+  key[i] = k;
+  // the host's copy (pinned memory, written across PCIe while the kernel
+  // runs): no separate copy kernel beside the index build
+  if (hkey) hkey[i] = k;
   uint32_t off, gv;
   uint64_t f;
   first_anchor(data, av, c, W, off, gv, f);
@@ -2667,7 +2670,7 @@ static int cu_count() {
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
                              uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
   if (!ntiles) return hipSuccess;
-  // the tiles' wave-tiles, a wave each at a time, three workgroups per CU
+  // the tiles' wave-tiles, a wave each at a time, kScanWgPerCu workgroups per CU
   const uint64_t wt0 = tile0 * (ZC_SCAN_TPB / 64), nwt = ntiles * (ZC_SCAN_TPB / 64);
   const unsigned grid = (unsigned)std::min<uint64_t>((nwt + kScanWaves - 1) / kScanWaves,
                                                      (uint64_t)cu_count() * kScanWgPerCu);
@@ -2715,7 +2718,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
   const uint64_t threads = std::max<uint64_t>({nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
                      nsref, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
-                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ec);
+                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ix.hkey, ec);
   if (after_meta) {
     const hipError_t e = hipEventRecord(after_meta, s);
     if (e != hipSuccess) return e;
