@@ -6,6 +6,8 @@ cd "$(dirname "$0")"
 b() { hipcc --offload-arch=gfx950 -O3 -std=c++17 -Dzc=zc_$1 -DSCAN_ENTRY=scan_v_$1 $2 -c scan_variant.hip -o /tmp/sv_$1.o; }
 # (round 5 also measured 4 x 4 waves with lists of 64 / 48 entries: r05_scan_geom_ab.txt)
 # and 2 x 4 waves with 256-byte rounds (-DZC_ROUND_CFG=256): r05_scan_geom_ab2.txt
-b prod "" & b ls2k "-DZC_LSPAN_CFG=2048" & b ls2k_wg2 "-DZC_LSPAN_CFG=2048 -DZC_SCAN_WG_PER_CU_CFG=2" & b wg3 "-DZC_SCAN_WG_PER_CU_CFG=3" & wait
+# and 2 KiB lane spans (-DZC_LSPAN_CFG=2048): r05_scan_geom_ab3/4.txt
+# and 3 x 4 waves (-DZC_SCAN_WG_PER_CU_CFG=3): r05_scan_geom_ab4.txt
+b prod "" & b s2 "-DZC_SCAN_SLOTS_CFG=2" & b s2_wg1 "-DZC_SCAN_SLOTS_CFG=2 -DZC_SCAN_WG_PER_CU_CFG=1" & b contig "-DZC_CONTIG_PROBE_CFG=1" & wait
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -c scan_geom_ab.hip -o /tmp/scan_geom_ab.o
-hipcc --offload-arch=gfx950 -o $out /tmp/scan_geom_ab.o /tmp/sv_prod.o /tmp/sv_ls2k.o /tmp/sv_ls2k_wg2.o /tmp/sv_wg3.o
+hipcc --offload-arch=gfx950 -o $out /tmp/scan_geom_ab.o /tmp/sv_prod.o /tmp/sv_s2.o /tmp/sv_s2_wg1.o /tmp/sv_contig.o

@@ -9,12 +9,13 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 typedef hipError_t (*ScanFn)(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                              uint32_t, unsigned long long*);
 #define DECL(N) extern "C" hipError_t N(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t, unsigned long long*);
-DECL(scan_v_prod) DECL(scan_v_ls2k) DECL(scan_v_ls2k_wg2) DECL(scan_v_wg3)
+DECL(scan_v_prod) DECL(scan_v_s2) DECL(scan_v_s2_wg1) DECL(scan_v_contig)
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 __global__ void fill(uint8_t* d, uint64_t n) {
@@ -37,9 +38,9 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, n);
   struct V { const char* name; ScanFn f; uint64_t* blk; std::vector<float> t; unsigned long long pool; };
   std::vector<V> vs = {{"product (2 x 4 waves, list 144)", scan_v_prod, nullptr, {}, 0},
-                       {"3 x 4 waves, 2 KiB lane spans", scan_v_ls2k, nullptr, {}, 0},
-                       {"2 x 4 waves, 2 KiB lane spans", scan_v_ls2k_wg2, nullptr, {}, 0},
-                       {"3 x 4 waves, list 144", scan_v_wg3, nullptr, {}, 0}};
+                       {"2 x 4 waves, two ring slots", scan_v_s2, nullptr, {}, 0},
+                       {"1 x 4 waves, two ring slots", scan_v_s2_wg1, nullptr, {}, 0},
+                       {"contiguous 8 KiB wave-rounds (probe)", scan_v_contig, nullptr, {}, 0}};
   uint32_t *dbase, *dcnt, *prel, *pg; unsigned long long* cnt;
   CK(hipMalloc(&dbase, nwt * 4)); CK(hipMalloc(&dcnt, nwt * 4));
   CK(hipMalloc(&prel, nwt * wcap * 4)); CK(hipMalloc(&pg, nwt * wcap * 4)); CK(hipMalloc(&cnt, 64));
@@ -60,7 +61,7 @@ int main(int argc, char** argv) {
   bool same = true;
   for (auto& v : vs) {
     CK(hipMemcpy(h1.data(), v.blk, nblk * 8, hipMemcpyDeviceToHost));
-    same = same && h0 == h1;
+    if (!strstr(v.name, "(probe)")) same = same && h0 == h1;  // a timing probe hashes the wrong bytes
     std::sort(v.t.begin(), v.t.end());
     printf("%-34s median %7.3f ms  min %7.3f ms  %7.1f GB/s (min)  pool %llu\n", v.name, v.t[v.t.size() / 2], v.t[0],
            n / (v.t[0] * 1e6), v.pool);

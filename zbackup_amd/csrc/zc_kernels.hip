@@ -453,6 +453,15 @@ constexpr int kDigests = ZC_LSPAN / ZC_SPAN;     // span digests per lane span
 // re-primed from the 32 bytes before each half, so a lane's anchors and gear
 // values do not depend on the order.
 constexpr int kHalfRounds = kRounds / 2;
+// Timing probe for tools/ubench/scan_geom_ab.hip only (never set in the
+// product): the DMA reads each wave-round as one contiguous 8 KiB block
+// (rows 128 bytes apart) while the lanes hash as if it were their spans --
+// wrong digests and anchors, the staging cost of a contiguous layout under
+// the real per-byte work (DESIGN 4.1 experiment 22)
+#ifndef ZC_CONTIG_PROBE_CFG
+#define ZC_CONTIG_PROBE_CFG 0
+#endif
+constexpr bool kContigProbe = ZC_CONTIG_PROBE_CFG != 0;
 constexpr uint32_t kHalfSpan = ZC_LSPAN / 2;
 static_assert((kHalfRounds & (kHalfRounds - 1)) == 0 && kHalfRounds % (ZC_SPAN / ZC_ROUND) == 0, "half-span rotation");
 
@@ -475,9 +484,11 @@ __device__ __forceinline__ void stage_round(const uint8_t* __restrict__ data, ui
                                             const uint32_t (&lane_off)[kDmaRound], uint64_t tile, int r,
                                             uint32_t slot) {
   uint8_t* dst = ring + slot * (64 * ZC_ROUND);
-  const uint64_t at = tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)(r % kHalfRounds) * ZC_ROUND;
+  const uint64_t at = kContigProbe
+                          ? tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)r * 64 * ZC_ROUND
+                          : tile * ZC_STILE + (uint64_t)wave * 64 * ZC_LSPAN + (uint64_t)(r % kHalfRounds) * ZC_ROUND;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(data + at), (short)0, 64 * ZC_LSPAN, 0x00020000);
-  const uint32_t flip = r >= kHalfRounds ? kHalfSpan : 0u;
+  const uint32_t flip = !kContigProbe && r >= kHalfRounds ? kHalfSpan : 0u;
 #pragma unroll
   for (int j = 0; j < kDmaRound; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + j * 1024), 16, (int)(lane_off[j] ^ flip), 0, 0,
@@ -712,8 +723,14 @@ constexpr int kScanWaves = ZC_SCAN_WAVES;  // per workgroup (one per SIMD)
 #define ZC_SCAN_WG_PER_CU_CFG 2
 #endif
 constexpr int kScanWgPerCu = ZC_SCAN_WG_PER_CU_CFG;  // workgroups resident per CU
+// ring slots per wave: rounds in flight while a wave hashes one
+#ifndef ZC_SCAN_SLOTS_CFG
+#define ZC_SCAN_SLOTS_CFG 1
+#endif
+constexpr int kScanSlots = ZC_SCAN_SLOTS_CFG;
+static_assert(kScanSlots == 1 || kScanSlots == 2, "one or two ring slots");
 struct ScanLds {
-  uint8_t ring[kScanWaves][64 * ZC_ROUND];
+  uint8_t ring[kScanWaves][kScanSlots * 64 * ZC_ROUND];
   uint4 wdata[kScanWaves][ZC_WLIST];
   uint32_t wlist[kScanWaves][ZC_WLIST * 3];
 };
@@ -735,16 +752,20 @@ __device__ __forceinline__ void scan_body(
 #pragma unroll
   for (int j = 0; j < kDmaRound; ++j) {
     const uint32_t row = j * (1024 / ZC_ROUND) + lane / kPieces;
-    lane_off[j] = row * ZC_LSPAN + (row & 1) * kHalfSpan + ((lane % kPieces) ^ row_swizzle(row)) * 16;
+    lane_off[j] = kContigProbe ? row * ZC_ROUND + ((lane % kPieces) ^ row_swizzle(row)) * 16
+                               : row * ZC_LSPAN + (row & 1) * kHalfSpan + ((lane % kPieces) ^ row_swizzle(row)) * 16;
   }
   const uint32_t sw = row_swizzle(lane);  // read-side swizzle of this lane's row
   const uint32_t two = pk_two();          // the packed state's multiplier, in an SGPR
   const uint32_t hs = (lane & 1) * kHalfRounds;  // logical round r is physical round r ^ hs
   v4u32 warm[2] = {};                       // the 32 bytes before the next half span
+  // vector-memory instructions of round Rx's group (its DMA, and for a half's
+  // first round the two warm-up loads)
+  auto group = [&](uint32_t Rx) -> uint32_t { return kDmaRound + ((Rx % kRpt) % kHalfRounds == 0 ? 2u : 0u); };
   auto issue = [&](uint32_t Rx) {
     const uint32_t k = Rx / kRpt, r = Rx - k * kRpt;
     const uint64_t wt = wt0 + gw + (uint64_t)k * nw;
-    stage_round<kScanDmaAux>(data, myring, (uint32_t)(wt % kWpt), lane_off, wt / kWpt, (int)r, 0u);
+    stage_round<kScanDmaAux>(data, myring, (uint32_t)(wt % kWpt), lane_off, wt / kWpt, (int)r, Rx % kScanSlots);
     if (r % kHalfRounds == 0) {
       // span 0 of the stream has no bytes before it: it reads itself (unused)
       const uint64_t at = (wt << ZC_WT_SHIFT) + (uint64_t)lane * ZC_LSPAN + (uint64_t)(r ^ hs) * ZC_ROUND;
@@ -753,13 +774,24 @@ __device__ __forceinline__ void scan_body(
       warm[1] = global_read16(src + 16);
     }
   };
-  if (nR > 0) issue(0);
+  // after[i]: vector-memory instructions issued after the group of round
+  // R + i (in flight: rounds R .. R + kScanSlots - 1); the wait for round R is
+  // vmcnt(after[0]) -- the counter retires in issue order
+  uint32_t after[kScanSlots];
+#pragma unroll
+  for (int i = 0; i < kScanSlots; ++i) {
+    after[i] = 0;
+    if ((uint32_t)i < nR) {
+#pragma unroll
+      for (int j = 0; j < i; ++j) after[j] += group(i);
+      issue(i);
+    }
+  }
   ScanLane s{0, 0, 0};
   uint64_t bk[kDigests];
 #pragma unroll
   for (int t = 0; t < kDigests; ++t) bk[t] = 0;
   uint64_t span0 = 0;
-  uint32_t tail_stores = 0;  // global stores the last tile end left in flight
   uint32_t last = kNoEntry;  // this lane's newest entry in the wave's list
   uint32_t acc_pool = 0, acc_over = 0;  // wave-uniform: anchors stored, wave-tiles overflowed
 
@@ -768,10 +800,10 @@ __device__ __forceinline__ void scan_body(
     const uint32_t k = R / kRpt;
     const int r = (int)(R - k * kRpt);
     // round R (and, for a half's first round, its warm-up loads) has landed
-    // once only what was issued after it is outstanding: nothing, or before a
-    // wave-tile's first round the last tile end's stores
-    if (r == 0) wait_vmcnt_dyn(tail_stores);
-    else wait_vmcnt<0>();
+    // once only what was issued after it is outstanding: the later rounds in
+    // flight and the last tile end's stores
+    if (kScanSlots == 1 && r != 0) wait_vmcnt<0>();
+    else wait_vmcnt_dyn(after[0]);
     const uint32_t pr = (uint32_t)r ^ hs;  // the physical round in the lane span
     if (r == 0) {
       // a new wave-tile
@@ -800,11 +832,19 @@ __device__ __forceinline__ void scan_body(
 #pragma unroll
     for (int g = 0; g < kGroups; ++g)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) vg[g][p] = lds_read16(myring + lane * ZC_ROUND + (((4 * g + p) ^ sw) << 4));
-    wait_lgkmcnt<0>();  // the slot is read out: refill it with the next round
+      for (int p = 0; p < 4; ++p)
+        vg[g][p] = lds_read16(myring + (R % kScanSlots) * (64 * ZC_ROUND) + lane * ZC_ROUND + (((4 * g + p) ^ sw) << 4));
+    wait_lgkmcnt<0>();  // the slot is read out: refill it with round R + kScanSlots
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) ties(vg[g]);
-    if (R + 1 < nR) issue(R + 1);
+#pragma unroll
+    for (int i = 0; i + 1 < kScanSlots; ++i) after[i] = after[i + 1];
+    after[kScanSlots - 1] = 0;
+    if (R + kScanSlots < nR) {
+#pragma unroll
+      for (int i = 0; i + 1 < kScanSlots; ++i) after[i] += group(R + kScanSlots);
+      issue(R + kScanSlots);
+    }
 #pragma unroll
     for (int g = 0; g < kGroups; ++g)
 #pragma unroll
@@ -817,8 +857,11 @@ __device__ __forceinline__ void scan_body(
       for (int t = 0; t < kDigests; ++t) bk[t] = q == (uint32_t)t ? h : bk[t];
       s.hlo = s.hhi = 0;
     }
-    if (r == kRounds - 1)
-      tail_stores = scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
+    if (r == kRounds - 1) {
+      const uint32_t ns = scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
+#pragma unroll
+      for (int i = 0; i < kScanSlots; ++i) after[i] += ns;
+    }
   }
   if (lane == 0) {
     if (acc_pool) atomicAdd(&counters[CNT_POOL], (unsigned long long)acc_pool);
