@@ -300,6 +300,104 @@ def static_leg(torch, buf, local, ks=(300000, 2000000), nbytes=1 << 30, reps=3):
     return out
 
 
+def synthetic_meta(rng, k, W=W64):
+    """Anchor metadata of k chunks this process never holds (ids of a large
+    repository's earlier backups): first anchor at a random offset >= 63, a key
+    shaped like a real anchor's ({st(q-1), st(q)}, st(q) passing the anchor
+    test at W's rate), a random fingerprint -- entries that fill the historic
+    index and its probe filter but match no window of the stream."""
+    import numpy as np
+    from zbackup_amd import META_DTYPE, anchor_def
+    rate = 4096  # anchor_rate_inv(65536)
+    lo = 0x8000 - 0x10000 // rate
+    m = np.zeros(k, dtype=META_DTYPE)
+    m["size"] = W
+    m["anchor_def"] = anchor_def(W)
+    m["anchor"] = rng.integers(63, W, k, dtype=np.uint32)
+    st_q = rng.integers(lo, 0x8000, k, dtype=np.uint32)
+    m["gear"] = (st_q << 16) | rng.integers(0, 1 << 16, k, dtype=np.uint32)
+    m["fingerprint"] = rng.integers(0, 2**63, k, dtype=np.int64).astype(np.uint64)
+    return m
+
+
+def seeded_repo_leg(torch, buf, n, seed, local, reps=4):
+    """A non-empty repository opened by a new process (ChunkIndex::loadIndex,
+    chunk_index.cc:26-79, zbackup_base.cc:87-100) with the content-anchor
+    metadata an earlier backup exported beside its index (zc_export_chunk_meta ->
+    zc_seed_index_meta, ABI 5): a fresh context seeded with the ids and metadata
+    of an earlier context's backup of (i) the same 8 GiB stream (every chunk a
+    duplicate) and (ii) a different one (none), then the C2 stream backed up with
+    SHA-1 ids.  The first call on the context is timed apart (its buffers are
+    made then); the value is the best of `reps` calls, each from the seeded
+    index (zc_forget_stream_chunks drops what the previous call added)."""
+    import numpy as np
+    from zbackup_amd import BackupCreator
+    out = {"unit": "GiB/s", "stream_bytes": n, "chunk_max_size": W64,
+           "path": "ids + anchor metadata of an earlier context's backup -> zc_seed_index_meta on a fresh context "
+                   "-> zc_chunk_device with SHA-1 ids (historic index probed by content anchors; no per-byte screen)"}
+    other = torch.empty(n, dtype=torch.uint8, device=buf.device)
+    fill_stream(torch, other, n, "c2", seed + 1000003, local)
+    for label, src in (("same_stream", buf), ("other_stream", other)):
+        with BackupCreator(W64, device=local, sha1=True) as a:
+            a.chunk_device(src.data_ptr(), n)
+            recs = a.records()
+            meta = a.export_chunk_meta()
+        ids = recs[recs["kind"] == 0]
+        with BackupCreator(W64, device=local, sha1=True, timing=True) as b:
+            b.seed_index_meta(ids["sha1"], ids["rolling"], ids["size"], meta)
+            seeded = b.stats()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            b.chunk_device(buf.data_ptr(), n)
+            torch.cuda.synchronize()
+            first_ms = (time.perf_counter() - t1) * 1e3
+            ts = []
+            for _ in range(reps):
+                b.forget_stream_chunks()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                b.chunk_device(buf.data_ptr(), n)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t1)
+            st = b.stats()
+            kinds = b.records()["kind"]
+        out[label] = {"value": round(n / min(ts) / 2**30, 3), "ms": round(min(ts) * 1e3, 3),
+                      "first_call_ms": round(first_ms, 3), "seeded_ids": int(len(ids)),
+                      "hist_seeded": int(seeded["hist_seeded"]), "by_value": int(seeded["by_value"]),
+                      "dup_records": int((kinds == 1).sum()), "new_records": int((kinds == 0).sum()),
+                      "stages": stage_dict(st)}
+    del other
+    # a 2 M-id repository partly written by stock zbackup: 99 % of the ids with
+    # metadata (the historic index: 2 M entries), 1 % by value (the exact
+    # screen runs at every byte for them), on the first GiB
+    rng = np.random.default_rng(2000000)
+    k = 2_000_000
+    keys = rng.integers(1, 2**63, k, dtype=np.int64).astype(np.uint64)
+    shas = rng.integers(0, 256, (k, 16), dtype=np.uint8)
+    meta = synthetic_meta(rng, k)
+    meta["sha1"] = shas
+    meta["rolling"] = keys
+    nb = 1 << 30
+    for label, frac in (("ids_2000000_all_meta", 1.0), ("ids_2000000_99pct_meta", 0.99)):
+        with BackupCreator(W64, device=local, sha1=True, timing=True) as b:
+            b.seed_index_meta(shas, keys, W64, meta[: int(k * frac)])
+            seeded = b.stats()
+            b.chunk_device(buf.data_ptr(), nb)
+            ts = []
+            for _ in range(3):
+                b.forget_stream_chunks()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                b.chunk_device(buf.data_ptr(), nb)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t1)
+            st = b.stats()
+        out[label] = {"value": round(nb / min(ts) / 2**30, 3), "ms": round(min(ts) * 1e3, 3), "stream_bytes": nb,
+                      "hist_seeded": int(seeded["hist_seeded"]), "by_value": int(seeded["by_value"]),
+                      "screen_ms": round(st["fscan_ms"], 3), "stages": stage_dict(st)}
+    return out
+
+
 def bundle_leg(torch, buf, n, recs, world, local, cpu_sample):
     """Bundle writer offload (§8(f)-4) over the stream's saved chunks: Writer::add's
     bundling (2 MiB bundles), the payloads gathered on the device and lzo1x_1
@@ -607,6 +705,8 @@ def run_rank(args):
                               "stages": stage_dict(st5)}
             del other
             extras["incremental"] = inc
+            if args.config == "c2" and n == 8 << 30:
+                extras["seeded_repo"] = seeded_repo_leg(torch, buf, n, seed, local)
         # the stream starts in (pinned) host memory, as in zutils.cc:100-124:
         # rolling-hash ids and complete ChunkIds
         host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
@@ -728,6 +828,8 @@ def run_rank(args):
                 out[key] = e
         if "incremental" in extras:
             out["incremental_sha1"] = extras["incremental"]
+        if "seeded_repo" in extras:
+            out["seeded_repo_sha1"] = extras["seeded_repo"]
         for key in ("feed", "feed_sha1", "feed_sha1_inline_sha256"):
             if key in extras:
                 out[key] = extras[key]

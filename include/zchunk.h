@@ -16,6 +16,15 @@
  *                          (chunk.max_size = W: zbackup.proto:79, config.cc:266-282)
  *   zc_seed_index          ChunkIndex::loadIndex -> registerNewChunkId, the static
  *                          probe set of an existing repository   chunk_index.cc:26-79,163-182
+ *   zc_seed_index_meta     the same, with the content-anchor metadata a sidecar kept for
+ *                          the ids (so the anchor probe finds them, not the per-byte
+ *                          screen): loadIndex + the sidecar read beside it
+ *                                                                chunk_index.cc:26-79,163-182,
+ *                                                                zbackup_base.cc:87-100
+ *   zc_export_chunk_meta   that metadata for the chunks this context's streams added, for the
+ *                          sidecar written at ChunkStorage::Writer::commit
+ *                                                                chunk_storage.cc:61-90,
+ *                                                                chunk_index.cc:185-202
  *   zc_set_window          the ring of W + page bytes the creator reads through
  *                          (backup_creator.cc:28-37): the stream's bytes held in HBM
  *   zc_get_input_buffer    BackupCreator::getInputBuffer()       backup_creator.hh:78 / .cc:40-43
@@ -43,7 +52,7 @@
 extern "C" {
 #endif
 
-#define ZCHUNK_ABI_VERSION 4
+#define ZCHUNK_ABI_VERSION 5
 
 enum zc_status {
   ZC_OK = 0,
@@ -84,6 +93,26 @@ typedef struct {
   uint32_t reserved;
 } zc_seed;
 
+/* ABI 5: the content-anchor metadata of one W-byte chunk of an index.  The
+ * engine finds windows equal to indexed chunks by their first content anchor
+ * (DESIGN.md §2); chunks whose bytes it never held (a repository's earlier
+ * backups, known to ChunkIndex only by id) are otherwise screened for by key at
+ * every byte.  The metadata is a pure function of the chunk's bytes, so it never
+ * goes stale: a caller keeps it beside the repository's index, keyed by the
+ * ChunkId, and seeds it with the ids (zc_seed_index_meta).  Matches are still
+ * confirmed by rolling key + SHA-1 prefix, as ChunkIndex::findChunk confirms
+ * them (chunk_index.cc:119-143), whatever the metadata says. */
+#define ZC_META_NO_ANCHOR 0xFFFFFFFFu
+typedef struct {
+  uint8_t sha1[16];      /* ChunkId::cryptoHash */
+  uint64_t rolling;      /* ChunkId::rollingHash */
+  uint32_t size;         /* chunk size (W for every entry the engine exports) */
+  uint32_t anchor_def;   /* zc_anchor_def() of the engine that computed the entry */
+  uint32_t anchor;       /* offset of the chunk's first content anchor, ZC_META_NO_ANCHOR: none */
+  uint32_t gear;         /* the anchor's key */
+  uint64_t fingerprint;  /* the anchor's 64-bit fingerprint */
+} zc_chunk_meta;
+
 typedef struct {
   double scan_ms;        /* zc_scan kernel (HIP events on the context stream) */
   double resolve_ms;     /* everything after the scan: total_ms - scan_ms with ZC_FLAG_TIMING */
@@ -111,6 +140,9 @@ typedef struct {
   uint64_t respeculations; /* streams redone because a speculative key + SHA-1 class join proved wrong */
   /* ABI 4: */
   uint64_t chk_rebuilds;   /* the one-level static screen's check table rebuilt larger for an epoch's own keys */
+  /* ABI 5: */
+  uint64_t hist_seeded;    /* historic index entries seeded with anchor metadata (zc_seed_index_meta) */
+  uint64_t by_value;       /* index entries known by value only (the exact screen's key set) */
 } zc_stats;
 
 typedef struct zc_ctx zc_ctx;
@@ -118,6 +150,24 @@ typedef struct zc_ctx zc_ctx;
 int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags);
 int zc_destroy(zc_ctx* ctx);
 int zc_seed_index(zc_ctx* ctx, const zc_seed* seeds, size_t n);
+/* ABI 5.  Seed the ids of an existing index (as zc_seed_index) together with the
+ * metadata kept for them: an id whose entry in meta[0, nm) matches its full
+ * ChunkId and size W and carries this engine's anchor definition joins the
+ * historic index (found by the anchor probe); the other ids are seeded by value
+ * (the exact screen); meta entries for ids not in seeds are ignored (an id
+ * that is not in the index never matches).  Call before the context's first
+ * stream adds chunks to its index (or after zc_forget_stream_chunks):
+ * ZC_ERR_STATE otherwise. */
+int zc_seed_index_meta(zc_ctx* ctx, const zc_seed* seeds, size_t n, const zc_chunk_meta* meta, size_t nm);
+/* ABI 5.  The metadata of the W-byte chunks this context's streams added to its
+ * index (ZC_FLAG_SHA1: Writer::add -> ChunkIndex::addChunk; in the order they
+ * were added; not the seeded ones): *n_out = their count; ZC_ERR_ARG (with
+ * *n_out the count) when cap is smaller. */
+int zc_export_chunk_meta(const zc_ctx* ctx, zc_chunk_meta* out, size_t cap, size_t* n_out);
+/* the anchor definition of this build for chunk.max_size W (it names the gear,
+ * the anchor rate for W, the minimum anchor offset and the fingerprint);
+ * metadata of another definition is ignored when seeding */
+uint32_t zc_anchor_def(uint32_t chunk_max_size);
 
 /* Host feed (zero-copy contract of BackupCreator: fill getInputBuffer() with up
  * to getInputBufferSize() bytes, then report how many were written).
@@ -139,7 +189,12 @@ uint64_t zc_get_window(const zc_ctx* ctx);
 void* zc_get_input_buffer(zc_ctx* ctx);
 size_t zc_get_input_buffer_size(zc_ctx* ctx);
 int zc_handle_more_data(zc_ctx* ctx, size_t added);
-int zc_feed(zc_ctx* ctx, const void* host, size_t n); /* copying convenience form */
+/* copying convenience form: n bytes through getInputBuffer / handleMoreData in
+ * pieces.  A call of more than getInputBufferSize() bytes may resolve several
+ * window halves and slide the window between them, so take the records after
+ * every call of at most that size when their payload bytes are needed
+ * (bytes_to_emit, Writer::add), as the zero-copy loop does. */
+int zc_feed(zc_ctx* ctx, const void* host, size_t n);
 int zc_finish(zc_ctx* ctx);
 
 /* device-resident stream: d_data is a device pointer on the context's GPU,

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version_and_argument_errors(lib):
     import ctypes
-    assert lib.zc_abi_version() == 4
+    assert lib.zc_abi_version() == 5
     ctx = ctypes.c_void_p()
     assert lib.zc_create(None, 65536, 0, 0) == _lib.ZC_ERR_ARG
     assert lib.zc_create(ctypes.byref(ctx), 0, 0, 0) == _lib.ZC_ERR_ARG  # chunk.max_size 0
@@ -54,8 +54,26 @@ def test_record_layout_matches_header():
     import ctypes
     assert ctypes.sizeof(_lib.ZcRecord) == 40
     assert ctypes.sizeof(_lib.ZcSeed) == 32
-    from zbackup_amd.chunker import RECORD_DTYPE
+    assert ctypes.sizeof(_lib.ZcChunkMeta) == 48
+    from zbackup_amd.chunker import META_DTYPE, RECORD_DTYPE, SEED_DTYPE
     assert RECORD_DTYPE.itemsize == 40
+    assert SEED_DTYPE.itemsize == 32
+    assert META_DTYPE.itemsize == 48
+    for name, _ in _lib.ZcChunkMeta._fields_:
+        assert META_DTYPE.fields[name][1] == getattr(_lib.ZcChunkMeta, name).offset, name
+
+
+def test_chunk_meta_calls_without_a_gpu(lib):
+    """The ABI-5 index-metadata entry points: argument errors and the anchor
+    definition need no device (no context is made)."""
+    import ctypes
+    n = ctypes.c_size_t()
+    assert lib.zc_export_chunk_meta(None, None, 0, ctypes.byref(n)) == _lib.ZC_ERR_ARG
+    assert lib.zc_seed_index_meta(None, None, 0, None, 0) == _lib.ZC_ERR_ARG
+    d64, d4k = lib.zc_anchor_def(65536), lib.zc_anchor_def(4096)
+    assert d64 >> 16 == 0x5A41 and d64 & 0xFF == 12  # anchors at 1 in 4096 positions for W = 64 KiB
+    assert d4k != d64 and d4k & 0xFF == 8            # 1 in 256 for W = 4 KiB (~16 per chunk)
+    assert lib.zc_anchor_def(0) == 0
 
 
 def test_chunk_id_blob_and_framing():

@@ -19,7 +19,9 @@ EXPORTS = ["zc_create", "zc_destroy", "zc_seed_index", "zc_get_input_buffer",
            "zc_chunk_device", "zc_record_count", "zc_get_records", "zc_get_stats", "zc_reset",
            "zc_last_error", "zc_fill_splitmix64", "zc_abi_version", "zc_read_stream", "zc_chunk_host",
            "zc_forget_stream_chunks", "zc_set_window", "zc_get_window", "zc_take_records", "zc_sha256_create", "zc_sha256_add", "zc_sha256_finish", "zc_sha256_destroy", "zc_sha256_impl",
-           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_compress_host", "zc_lzo_last_stats", "zc_adler32", "zc_serialize_records", "zc_stream_data", "zc_build_id"]
+           "zc_bundle_plan", "zc_bundle_gather", "zc_lzo_capacity", "zc_lzo_compress", "zc_lzo_compress_host", "zc_lzo_last_stats", "zc_adler32", "zc_serialize_records", "zc_stream_data", "zc_build_id",
+           "zc_seed_index_meta", "zc_export_chunk_meta", "zc_anchor_def"]
+ZC_META_NO_ANCHOR = 0xFFFFFFFF
 
 
 class ZcRecord(ctypes.Structure):
@@ -30,6 +32,12 @@ class ZcRecord(ctypes.Structure):
 class ZcSeed(ctypes.Structure):
     _fields_ = [("sha1", ctypes.c_uint8 * 16), ("rolling", ctypes.c_uint64),
                 ("size", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class ZcChunkMeta(ctypes.Structure):
+    _fields_ = [("sha1", ctypes.c_uint8 * 16), ("rolling", ctypes.c_uint64), ("size", ctypes.c_uint32),
+                ("anchor_def", ctypes.c_uint32), ("anchor", ctypes.c_uint32), ("gear", ctypes.c_uint32),
+                ("fingerprint", ctypes.c_uint64)]
 
 
 class ZcStats(ctypes.Structure):
@@ -43,7 +51,8 @@ class ZcStats(ctypes.Structure):
                 ("window_bytes", ctypes.c_uint64), ("hbm_bytes", ctypes.c_uint64),
                 ("segments", ctypes.c_uint64), ("hist_entries", ctypes.c_uint64),
                 ("sha_wait_ms", ctypes.c_double), ("sha_fill_ms", ctypes.c_double), ("hist_ms", ctypes.c_double),
-                ("respeculations", ctypes.c_uint64), ("chk_rebuilds", ctypes.c_uint64)]
+                ("respeculations", ctypes.c_uint64), ("chk_rebuilds", ctypes.c_uint64),
+                ("hist_seeded", ctypes.c_uint64), ("by_value", ctypes.c_uint64)]
 
 
 class ZcError(RuntimeError):
@@ -108,6 +117,9 @@ def load(path=LIB_PATH):
         "zc_lzo_last_stats": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]),
         "zc_stream_data": (vp, [vp, u64, sz]),
         "zc_build_id": (ctypes.c_char_p, []),
+        "zc_seed_index_meta": (i32, [vp, vp, sz, vp, sz]),
+        "zc_export_chunk_meta": (i32, [vp, vp, sz, ctypes.POINTER(sz)]),
+        "zc_anchor_def": (u32, [u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

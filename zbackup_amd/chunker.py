@@ -21,6 +21,10 @@ from . import _lib
 RECORD_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u4"), ("kind", "<u4"),
                          ("rolling", "<u8"), ("sha1", "u1", (16,))])
 KIND_CHAR = "NDB"
+SEED_DTYPE = np.dtype([("sha1", np.uint8, 16), ("rolling", np.uint64), ("size", np.uint32), ("reserved", np.uint32)])
+# zc_chunk_meta (ABI 5): a chunk's content-anchor metadata, keyed by its ChunkId
+META_DTYPE = np.dtype([("sha1", np.uint8, 16), ("rolling", "<u8"), ("size", "<u4"), ("anchor_def", "<u4"),
+                       ("anchor", "<u4"), ("gear", "<u4"), ("fingerprint", "<u8")])
 
 
 def _check(L, ctx, rc, what):
@@ -51,6 +55,24 @@ def serialize_instruction(chunk_blob=None, raw=None):
     if raw is not None:
         body += b"\x12" + _varint(len(raw)) + raw
     return _varint(len(body)) + body
+
+
+def _seed_array(sha1, rolling, size):
+    """(sha1 (n, 16) uint8, rolling (n,) uint64, size scalar or (n,)) -> SEED_DTYPE array (zc_seed)."""
+    rolling = np.ascontiguousarray(rolling, dtype=np.uint64).reshape(-1)
+    n = rolling.size
+    rec = np.zeros(n, dtype=SEED_DTYPE)
+    assert rec.dtype.itemsize == ctypes.sizeof(_lib.ZcSeed)
+    if n:
+        rec["sha1"] = np.asarray(sha1, dtype=np.uint8).reshape(n, 16)
+        rec["rolling"] = rolling
+        rec["size"] = size
+    return rec
+
+
+def anchor_def(chunk_max_size):
+    """zc_anchor_def: the anchor definition this build's metadata carries for W."""
+    return int(_lib.load().zc_anchor_def(int(chunk_max_size)))
 
 
 class BackupCreator:
@@ -92,18 +114,38 @@ class BackupCreator:
         """seed_index for ids given as arrays: sha1 (n, 16) uint8, rolling (n,)
         uint64, size a scalar or (n,) -- one copy into the ZcSeed array (an
         index file's worth of ids without a Python loop)."""
-        rolling = np.ascontiguousarray(rolling, dtype=np.uint64)
-        n = rolling.size
-        if n == 0:
+        rec = _seed_array(sha1, rolling, size)
+        if rec.size == 0:
             return
-        rec = np.zeros(n, dtype=np.dtype([("sha1", np.uint8, 16), ("rolling", np.uint64), ("size", np.uint32),
-                                          ("reserved", np.uint32)]))
-        assert rec.dtype.itemsize == ctypes.sizeof(_lib.ZcSeed)
-        rec["sha1"] = np.asarray(sha1, dtype=np.uint8).reshape(n, 16)
-        rec["rolling"] = rolling
-        rec["size"] = size
-        arr = (_lib.ZcSeed * n).from_buffer(rec)
-        _check(self._L, self._ctx, self._L.zc_seed_index(self._ctx, arr, n), "zc_seed_index")
+        arr = (_lib.ZcSeed * rec.size).from_buffer(rec)
+        _check(self._L, self._ctx, self._L.zc_seed_index(self._ctx, arr, rec.size), "zc_seed_index")
+
+    def seed_index_meta(self, sha1, rolling, size, meta):
+        """zc_seed_index_meta: the ids of an existing index (arrays as in
+        seed_index_arrays) with the anchor metadata kept for them (a META_DTYPE
+        array, e.g. from export_chunk_meta of the backups that wrote them).  Ids
+        whose metadata matches join the anchor-probed historic index, the rest
+        are seeded by value; metadata of ids not given is ignored."""
+        rec = _seed_array(sha1, rolling, size)
+        meta = np.ascontiguousarray(meta, dtype=META_DTYPE)
+        assert META_DTYPE.itemsize == ctypes.sizeof(_lib.ZcChunkMeta)
+        _check(self._L, self._ctx,
+               self._L.zc_seed_index_meta(self._ctx, rec.ctypes.data if rec.size else None, rec.size,
+                                          meta.ctypes.data if meta.size else None, meta.size),
+               "zc_seed_index_meta")
+
+    def export_chunk_meta(self):
+        """zc_export_chunk_meta: the anchor metadata of the W-byte chunks this
+        context's streams added to its index (ZC_FLAG_SHA1), as a META_DTYPE
+        array in the order they were added."""
+        need = ctypes.c_size_t()
+        self._L.zc_export_chunk_meta(self._ctx, None, 0, ctypes.byref(need))
+        out = np.zeros(need.value, dtype=META_DTYPE)
+        if need.value:
+            _check(self._L, self._ctx,
+                   self._L.zc_export_chunk_meta(self._ctx, out.ctypes.data, out.size, ctypes.byref(need)),
+                   "zc_export_chunk_meta")
+        return out
 
     def _new_stream(self):
         # A fed stream's records are taken from the context as they are cut and
@@ -157,9 +199,23 @@ class BackupCreator:
         self._drain()
 
     def feed(self, data):
+        """The read loop of zutils.cc:100-124 over `data`: each piece copied into
+        getInputBuffer() (at most getInputBufferSize() bytes), handleMoreData,
+        and the records cut by then taken and serialized while their payload
+        bytes are still in the feed window (a long stream slides the window on
+        the next getInputBuffer call)."""
         data = np.ascontiguousarray(np.frombuffer(memoryview(data), dtype=np.uint8))
-        _check(self._L, self._ctx, self._L.zc_feed(self._ctx, data.ctypes.data, data.size), "zc_feed")
-        self._drain()
+        pos = 0
+        while pos < data.size:
+            p = self._L.zc_get_input_buffer(self._ctx)
+            room = self._L.zc_get_input_buffer_size(self._ctx)
+            if not p or not room:
+                msg = self._L.zc_last_error(self._ctx) or b""
+                raise _lib.ZcError(f"getInputBuffer failed: {msg.decode(errors='replace')}")
+            take = min(room, data.size - pos)
+            ctypes.memmove(p, data.ctypes.data + pos, take)
+            self.handle_more_data(take)
+            pos += take
 
     def finish(self):
         _check(self._L, self._ctx, self._L.zc_finish(self._ctx), "finish")

@@ -327,6 +327,35 @@ hipError_t launch_probe(const uint8_t* data, AnchorView av, uint64_t wt0, uint64
                         const HistTab& ht, uint64_t r_e, uint32_t nconf, uint32_t nspec, Cand* cand,
                         uint64_t cand_cap, unsigned long long* counters, hipStream_t s);
 
+// The probe's candidates split and ordered on the device (zc_cand_split, a
+// three-launch bucket scan, zc_cand_scatter, zc_bucket_sort): epoch
+// candidates (pad 0) appended to out0 (count hc[3]); historic ones whose
+// window key equals hkey[ref] to out in position order (count hc[1]; pad 1:
+// the window is a grid chunk q W, q < n_gsha, whose SHA-1 the side stream
+// computes; 2: not), unless hc[2] != 0: a bucket too large to sort on the
+// device (the host sorts out by p then).  Buckets are p >> bshift,
+// nb = (n >> bshift) + 1 <= 2^20 of them.  Scratch: bcnt (nb, all zero
+// between calls: zero it when made), boff (nb + 1), bsum (nb / 1024 + 1),
+// rank (nc), hc (4, zero when made; the calls keep it so).  Results land in
+// the pinned host buffers h_out0 / h_out / h_hc (no runtime copies).
+struct CandOrderBufs {
+  uint32_t bshift, nb;
+  uint32_t* bcnt;
+  uint32_t* boff;
+  uint32_t* bsum;
+  uint32_t* rank;
+  Cand* out0;
+  Cand* out;
+  unsigned long long* hc;
+  // pinned host memory the results are written to (nc entries each, 4 counters)
+  Cand* h_out0;
+  Cand* h_out;
+  unsigned long long* h_hc;
+};
+hipError_t launch_cand_order(const uint8_t* data, const uint64_t* blk, const Cand* cand, uint32_t nc,
+                             const uint64_t* hkey, uint64_t pw, uint32_t W, uint64_t n, uint64_t n_gsha,
+                             CandOrderBufs b, hipStream_t s);
+
 hipError_t launch_verify_pairs(const uint8_t* data, const uint64_t* win_start,
                                const uint64_t* ref_start, uint32_t len, uint32_t npairs,
                                uint8_t* ok, hipStream_t s);

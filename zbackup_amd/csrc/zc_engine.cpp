@@ -211,8 +211,14 @@ class SpinTeam {
     if (!team || owner != getpid()) {
       team = new SpinTeam;
       owner = getpid();
+      live_.store(team, std::memory_order_release);
     }
     return *team;
+  }
+  // disarm() on the team if this process has one (none is made for it)
+  static void disarm_any() {
+    SpinTeam* t = live_.load(std::memory_order_acquire);
+    if (t) t->disarm();
   }
   // the helpers spin for at most `ms` from now
   void arm(double ms = 8.0) {
@@ -223,6 +229,9 @@ class SpinTeam {
     }
     cv_.notify_all();
   }
+  // the helpers stop spinning now (the jobs they were armed for are done):
+  // they do not compete with the caller's host work until the next arm()
+  void disarm() { deadline_.store(0, std::memory_order_relaxed); }
   // f(begin, end) over [0, n) in kParts parts; the helpers that are not
   // spinning (not armed, or past the deadline) are not waited for: their
   // parts run on this thread
@@ -286,6 +295,7 @@ class SpinTeam {
       }
     }
   }
+  static inline std::atomic<SpinTeam*> live_{nullptr};
   std::vector<std::thread> th_;
   std::mutex run_, m_;
   std::condition_variable cv_;
@@ -408,10 +418,13 @@ struct zc_ctx {
   std::vector<uint64_t, DefaultInit<uint64_t>> hkey;  // (resize leaves new entries to be written)
   std::vector<uint8_t, DefaultInit<uint8_t>> hsha;  // 16 bytes per entry (resize leaves them to be written)
   uint32_t nhist = 0;
+  uint32_t nhist_seeded = 0;  // entries [0, nhist_seeded) came from zc_seed_index_meta
   DevBuf<uint32_t> hanc, hg;
   DevBuf<uint64_t> hfp, htab;
+  DevBuf<uint64_t> hkey_d;  // the entries' keys on the device too (the candidates' key check)
   DevBuf<uint32_t> hfilt;
   uint32_t hbits = 0;
+  bool hist_dirty = false;  // the table holds entries no longer in the index: rebuild before use
 
   // records: recs[rec_head, nrec_done) are complete (digests and chunk ids
   // filled in) and not yet taken (zc_take_records); records past nrec_done are
@@ -433,6 +446,12 @@ struct zc_ctx {
   // pages later (the list's destructor) stalled the next call's first
   // submission by 8-28 ms on the GPU box
   HostBuf<Cand> h_cand;
+  // the candidates' device split and ordering (launch_cand_order)
+  DevBuf<uint32_t> co_bcnt, co_boff, co_bsum, co_rank;
+  DevBuf<Cand> co_out0, co_out;
+  DevBuf<unsigned long long> co_hc;
+  HostBuf<unsigned long long> h_co_hc;
+  HostBuf<Cand> h_hist_cand;  // the historic candidates, key-checked and in position order
   HostBuf<uint32_t> h_cls;  // the epoch's content classes (likewise)
   HostBuf<Run> h_runs;      // the screen's runs (likewise)
   size_t nrec_done = 0;
@@ -559,8 +578,11 @@ void statics_screen(zc_ctx& c) {
     // after an epoch overflowed it); a chain that would reach the last bucket
     // makes the table twice as large.  (ZC_TEST_CHK_BITS: tests start the
     // search from a table too small for any epoch keys, to force that overflow.)
+    // (the hook's value is used only inside [10, 30]; anything else is ignored)
     const char* tb = c.chk_room == kChkRoomDefault ? getenv("ZC_TEST_CHK_BITS") : nullptr;
-    for (c.chk_bits = tb ? (uint32_t)atoi(tb) : chk_bits_for(keys.size() + c.chk_room);; ++c.chk_bits) {
+    const long tbv = tb ? strtol(tb, nullptr, 10) : 0;
+    const bool test_bits = tbv >= 10 && tbv <= 30;
+    for (c.chk_bits = test_bits ? (uint32_t)tbv : chk_bits_for(keys.size() + c.chk_room);; ++c.chk_bits) {
       const uint64_t nb = (1ull << c.chk_bits) + kChkPad;
       std::vector<uint16_t> chk(nb * 4, 0);
       bool fits = true;
@@ -589,14 +611,18 @@ void statics_screen(zc_ctx& c) {
   c.sc_ver = c.statics_ver;
 }
 
-// historic table: 2^hbits >= 2 nhist slots; grows by a rebuild, otherwise
-// entries [from, nhist) are inserted
-void hist_table(zc_ctx& c, uint32_t from) {
-  if (!c.nhist) return;
+// historic table: 2^hbits >= 2 max(nhist, room) slots; grows by a rebuild
+// (or is rebuilt at its size with `clear`), otherwise entries [from, nhist)
+// are inserted
+void hist_table(zc_ctx& c, uint32_t from, uint64_t room = 0, bool clear = false) {
+  const uint64_t want = std::max<uint64_t>(c.nhist, room);
+  if (clear) c.hist_dirty = true;
+  if (!want) return;  // (an empty index is not probed: cleared when it is next filled)
   uint32_t bits = std::max<uint32_t>(c.hbits, 12);
-  while ((1ull << bits) < 2ull * c.nhist) ++bits;
+  while ((1ull << bits) < 2ull * want) ++bits;
   c.hfilt.ensure(probe_filter_words());
-  if (bits != c.hbits || !c.htab.p) {
+  if (bits != c.hbits || !c.htab.p || c.hist_dirty) {
+    c.hist_dirty = false;
     sync(c);  // a probe may still read the old table
     c.htab.ensure(2ull << bits);
     c.hbits = bits;
@@ -604,8 +630,34 @@ void hist_table(zc_ctx& c, uint32_t from) {
     HCK(hipMemsetAsync(c.htab.p, 0xFF, (2ull << bits) * sizeof(uint64_t), c.stream));
     HCK(hipMemsetAsync(c.hfilt.p, 0, probe_filter_words() * sizeof(uint32_t), c.stream));
   }
-  HCK(launch_hist_insert(c.hg.p, c.hfp.p, c.hanc.p, from, c.nhist - from, c.htab.p, c.hbits, c.hfilt.p, c.stream));
+  if (c.nhist > from)
+    HCK(launch_hist_insert(c.hg.p, c.hfp.p, c.hanc.p, from, c.nhist - from, c.htab.p, c.hbits, c.hfilt.p, c.stream));
 }
+
+// Room for `total` historic entries, made before a stream queues any work:
+// the device arrays and the table are grown now, since growing them when the
+// stream's new chunks register at its end frees the old buffers, and hipFree
+// waits for the whole device -- the grid SHA-1 on its side stream included
+// (the registration's cost then followed the history's size: 1.70 ms with
+// 131,072 entries, 0.23 with none).  Grown geometrically, so a
+// long series of backups on one context rebuilds its table O(log) times.
+void hist_reserve(zc_ctx& c, uint64_t total) {
+  if (total > 0xFFFFFFF0ull || total <= c.nhist) return;
+  if (total > c.hanc.cap) total = std::max<uint64_t>(total, 2ull * c.nhist);
+  c.hanc.grow_keep(total, c.nhist, c.stream);
+  c.hg.grow_keep(total, c.nhist, c.stream);
+  c.hfp.grow_keep(total, c.nhist, c.stream);
+  c.hkey_d.grow_keep(total, c.nhist, c.stream);
+  c.hkey.reserve(total);
+  c.hsha.reserve(16 * total);
+  hist_table(c, c.nhist, total);
+}
+
+// the anchor definition metadata carries (zc_anchor_def): 'ZA', definition 2
+// (two packed 16-bit parity gears tested at every byte, the first anchor at
+// offset >= ZC_ANCHOR_MIN_OFF, the 8-byte fingerprint ending at it: round 5),
+// and log2 of the anchor rate chosen for W
+uint32_t anchor_def_of(uint32_t W) { return 0x5A410000u | (2u << 8) | (uint32_t)__builtin_ctz(anchor_rate_inv(W)); }
 
 // a by-value entry unless (key, SHA-1) is indexed already (registerNewChunkId,
 // chunk_index.cc:163-182)
@@ -627,8 +679,7 @@ void index_truncate(zc_ctx& c, uint32_t nh, size_t ns, bool force = false) {
   c.smap.clear();
   for (uint32_t i = 0; i < c.statics.size(); ++i) c.smap[c.statics[i].key].push_back(i);
   ++c.statics_ver;
-  c.hbits = 0;  // rebuilt
-  hist_table(c, 0);
+  hist_table(c, 0, 0, true);  // rebuilt at its size (the next stream needs the room again)
 }
 
 // ---------------------------------------------------------------------------
@@ -681,6 +732,9 @@ class Resolver {
     c_.stats.window_bytes = windowed_ ? c_.win_cap : 0;
     hist0_ = c_.nhist;
     statics0_ = c_.statics.size();
+    // the stream's new W-byte chunks (at most n / W of them) join the index at
+    // its end: room for them now, before anything of the stream is queued
+    if (!windowed_ && indexable_ && (c_.flags & ZC_FLAG_SHA1) && n_ >= W_) hist_reserve(c_, c_.nhist + n_ / W_ + 2);
     r_ = s_ = x_resume_ = hspan_ = 0;
     gruns_.clear();
     fresh_.clear();
@@ -703,6 +757,7 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
+      scan_counters_clear();
       HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
                             c_.stream));
       tiles_done_ = t1;
@@ -743,6 +798,7 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
+      scan_counters_clear();
       HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.counters.p, c_.stream));
       if (!windowed_) pre_sha();
       scan_finish();
@@ -843,6 +899,7 @@ class Resolver {
     c_.hanc.grow_keep(e0 + k, e0, c_.stream);
     c_.hg.grow_keep(e0 + k, e0, c_.stream);
     c_.hfp.grow_keep(e0 + k, e0, c_.stream);
+    c_.hkey_d.grow_keep(e0 + k, e0, c_.stream);
     c_.h_hmanc.ensure(k);
     // a leading run of consecutive grid chunks of the epoch whose metadata the
     // device arrays hold (a whole stream's new chunks, but for the last one or
@@ -860,6 +917,8 @@ class Resolver {
       HCK(hipMemcpyAsync(c_.hanc.p + e0, c_.c_anc.p + r0, run * sizeof(uint32_t), hipMemcpyDeviceToDevice, c_.stream));
       HCK(hipMemcpyAsync(c_.hg.p + e0, c_.c_g.p + r0, run * sizeof(uint32_t), hipMemcpyDeviceToDevice, c_.stream));
       HCK(hipMemcpyAsync(c_.hfp.p + e0, c_.c_fp.p + r0, run * sizeof(uint64_t), hipMemcpyDeviceToDevice, c_.stream));
+      HCK(hipMemcpyAsync(c_.hkey_d.p + e0, c_.c_key.p + r0, run * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                         c_.stream));
       memcpy(c_.hkey.data() + e0, c_.h_key.p + (r0 - dev_nconf_), run * sizeof(uint64_t));
     }
     if (run < k) {
@@ -909,6 +968,7 @@ class Resolver {
                               c_.hanc.p + eb, c_.hg.p + eb, c_.hfp.p + eb, c_.stream));
       }
       c_.h_hmkey.ensure(kr);
+      HCK(hipMemcpyAsync(c_.hkey_d.p + eb, c_.hm_key.p, kr * sizeof(uint64_t), hipMemcpyDeviceToDevice, c_.stream));
       d2h(c_, c_.h_hmkey.p, c_.hm_key.p, kr);
       sync(c_);
       memcpy(c_.hkey.data() + eb, c_.h_hmkey.p, kr * sizeof(uint64_t));
@@ -1150,8 +1210,10 @@ class Resolver {
     const uint64_t found = c_.h_scnt[CNT_POOL];
     npool_ += found;
     c_.stats.anchors += found;
-    // the next scan launch counts from zero
-    HCK(hipMemsetAsync(c_.counters.p, 0, 2 * sizeof(unsigned long long), c_.stream));
+    // the next scan launch counts from zero (cleared right before it, if one
+    // comes: a fill queued here ran beside the grid SHA-1 at its priority and
+    // held up the epoch's own device work by ~25 us)
+    scan_counters_dirty_ = true;
     if (c_.h_scnt[CNT_OVERFLOW] && wt_hi > wt_lo) {
       // wave-tiles whose anchors overflowed the scan's LDS list or their pool
       // share (dense data): count them exactly, then rescan into a side pool
@@ -1190,6 +1252,12 @@ class Resolver {
     return false;
   }
   bool scan_checked_ = true;
+  bool scan_counters_dirty_ = false;
+  void scan_counters_clear() {
+    if (!scan_counters_dirty_) return;
+    scan_counters_dirty_ = false;
+    HCK(hipMemsetAsync(c_.counters.p, 0, 2 * sizeof(unsigned long long), c_.stream));
+  }
   bool meta_from_scan_ = false;  // ev1 marks the end of scan launches queued for this batch
   hipEvent_t side_wait_ = nullptr;  // the copy stream's next work waits for this scan end
 
@@ -1294,7 +1362,6 @@ class Resolver {
         HCK(launch_probe(d_, av(), pwt0(), pwt1() - pwt0(), tab, tbits, c_.gfilt.p, c_.c_anc.p, c_.c_cls.p,
                          c_.c_vis.p, c_.c_dead.p, r_, h_end_, W_, ht, r_e_, nconf_, nsref, c_.cand.p, c_.cand.cap, c_.counters.p,
                          c_.stream));
-      sha_launch();
       // (the grid chunks' keys reach the host from the metadata kernel itself;
       // the tail digests below need the scan's span digests)
       if (side_wait_) {
@@ -1308,6 +1375,9 @@ class Resolver {
       const bool first = !scan_checked_ && meta_from_scan_;  // this batch also waits for the scan
       if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
       d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
+      // the grid SHA-1 behind the batch's read-back too: that copy runs alone
+      // (beside the SHA-1 it took 14 us instead of 6), the SHA-1 a few us later
+      sha_launch();
       sync(c_);
       HCK(hipStreamSynchronize(c_.copy_stream));
       if (scan_check()) {  // the pool changed under this epoch: queue it again
@@ -1447,28 +1517,26 @@ class Resolver {
   // as ChunkIndex::findChunk confirms them (chunk_index.cc:119-143)
   void verify_candidates(uint64_t nc) {
     c_.stats.candidates += nc;
+    if (c_.nhist) {
+      verify_candidates_dev(nc);
+      return;
+    }
     c_.h_cand.ensure(nc);
-    const Cand* const hc = c_.h_cand.p;
     d2h(c_, c_.h_cand.p, c_.cand.p, nc);
     sync(c_);
+    verify_epoch_cands(c_.h_cand.p, nc);
+  }
+
+  // candidates of this epoch's refs (hc[0, m), all pad 0) -> acands_
+  void verify_epoch_cands(const Cand* hc, uint64_t m) {
     // a window that is exactly a grid chunk of this epoch in the candidate's
     // class is already known equal (the class was byte-verified)
     std::vector<uint64_t> wa, ra;
     std::vector<uint64_t> idx;
     std::vector<uint8_t>& ok = c_.res_ok;
-    ok.assign(nc, 1);
-    std::vector<uint64_t>& ha = c_.res_ha;  // historic candidates' windows [ha, ha + W)
-    std::vector<uint64_t>& hidx = c_.res_hidx;
-    ha.clear();
-    hidx.clear();
-    for (uint64_t i = 0; i < nc; ++i) {
+    ok.assign(m, 1);
+    for (uint64_t i = 0; i < m; ++i) {
       const uint64_t ws = hc[i].p - W_ + 1;
-      if (hc[i].pad) {
-        ok[i] = 0;
-        ha.push_back(ws);
-        hidx.push_back(i);
-        continue;
-      }
       if (!cls_.empty() && ws >= r_e_ && wmod(ws - r_e_) == 0 && wdiv(ws - r_e_) < nref_ - nconf_) {
         const uint32_t r = nconf_ + (uint32_t)wdiv(ws - r_e_);
         if (cls_[r] == hc[i].ref) continue;
@@ -1479,53 +1547,90 @@ class Resolver {
     }
     std::vector<uint8_t> vok = verify_pairs(wa, ra, W_);
     for (size_t j = 0; j < idx.size(); ++j) ok[idx[j]] = vok[j];
-    if (!hidx.empty()) {
-      const uint64_t* const key = window_digests(ha);
-      hcands_.reserve(hcands_.size() + hidx.size());
-      if (spec_) spec_hist_.reserve(spec_hist_.size() + hidx.size());
-      std::vector<uint64_t> sa;
-      std::vector<uint32_t> sl;
-      std::vector<size_t> sidx;
-      for (size_t j = 0; j < hidx.size(); ++j)
-        if (key[j] == c_.hkey[hc[hidx[j]].ref]) {
-          // a window that is a grid chunk has its SHA-1 from the speculative
-          // grid pass (the incremental backup of unchanged data: all of them)
-          if (spec_ && grid_sha_pending(ha[j])) {
-            // speculatively (whole-stream SHA-1 mode): joined on the key now,
-            // the SHA-1 prefixes compared once the grid digests land
-            // (finalize_records; a mismatch redoes the stream without
-            // speculation), so the walk need not wait for the grid SHA-1
-            const uint64_t i = hidx[j];
-            hcands_.push_back({hc[i].p, hc[i].ref});
-            spec_hist_.push_back({wdiv(ha[j]), hc[i].ref});
-            continue;
-          }
-          if (const uint8_t* g = grid_sha_of(ha[j])) {
-            const uint64_t i = hidx[j];
-            if (memcmp(g, &c_.hsha[16 * (size_t)hc[i].ref], 16) == 0) hcands_.push_back({hc[i].p, hc[i].ref});
-            continue;
-          }
-          sa.push_back(ha[j]);
-          sl.push_back(W_);
-          sidx.push_back(j);
-        }
+    acands_.reserve(acands_.size() + m);
+    for (uint64_t i = 0; i < m; ++i)
+      if (ok[i]) acands_.push_back({hc[i].p, hc[i].ref});
+    sort_by_position(acands_);
+  }
+
+  // With a historic index the candidates are split on the device: the epoch's
+  // come back as a list of their own, the historic ones key-checked and in
+  // position order (launch_cand_order), so the host reads each once, in order
+  void verify_candidates_dev(uint64_t nc) {
+    if (nc > 0xFFFFFFF0ull) throw ZcError{ZC_ERR_NOMEM, "too many probe candidates"};
+    // buckets of ~n / (2 nc) positions: a few candidates each at most
+    // (at most 2^20 buckets: the scan's block sums fit one workgroup)
+    uint32_t bshift = 0;
+    const uint64_t nb_max = std::min<uint64_t>(std::max<uint64_t>(2 * nc, 1024), 1u << 20);
+    while (bshift < 63 && (n_ >> bshift) + 1 > nb_max) ++bshift;
+    const uint32_t nb = (uint32_t)((n_ >> bshift) + 1);
+    // the bucket counts and the call counters stay zero between calls (the
+    // kernels clear them): filled only when (re)made
+    if (c_.co_bcnt.cap < nb || !c_.co_bcnt.p) {
+      c_.co_bcnt.ensure(std::max<uint64_t>(nb, 1u << 16));
+      HCK(hipMemsetAsync(c_.co_bcnt.p, 0, c_.co_bcnt.cap * sizeof(uint32_t), c_.stream));
+    }
+    if (!c_.co_hc.p) {
+      c_.co_hc.ensure(4);
+      HCK(hipMemsetAsync(c_.co_hc.p, 0, 4 * sizeof(unsigned long long), c_.stream));
+    }
+    c_.co_boff.ensure((uint64_t)nb + 1);
+    c_.co_bsum.ensure((uint64_t)nb / 1024 + 2);
+    c_.co_rank.ensure(nc);
+    c_.co_out0.ensure(nc);
+    c_.co_out.ensure(nc);
+    c_.h_co_hc.ensure(4);
+    c_.h_cand.ensure(nc);
+    c_.h_hist_cand.ensure(nc);
+    const CandOrderBufs b{bshift,       nb,          c_.co_bcnt.p,  c_.co_boff.p,       c_.co_bsum.p,
+                          c_.co_rank.p, c_.co_out0.p, c_.co_out.p, c_.co_hc.p,         c_.h_cand.p,
+                          c_.h_hist_cand.p, c_.h_co_hc.p};
+    HCK(launch_cand_order(d_, blk_v(), c_.cand.p, (uint32_t)nc, c_.hkey_d.p, pow257(W_), W_, n_,
+                          pre_sha_n_ ? pre_sha_n_ : 0, b, c_.stream));
+    sync(c_);
+    const uint64_t n0 = c_.h_co_hc[3], nk = c_.h_co_hc[1];
+    const bool unsorted = c_.h_co_hc[2] != 0;
+    if (n0) verify_epoch_cands(c_.h_cand.p, n0);
+    if (!nk) return;
+    Cand* const hk = c_.h_hist_cand.p;
+    if (unsorted) std::stable_sort(hk, hk + nk, [](const Cand& x, const Cand& y) { return x.p < y.p; });
+    // the windows that are no grid chunk of the side stream's SHA-1 pass
+    // (pad 2) are hashed here, in batches; the rest are grid chunks: joined on
+    // the key now and checked when the digests land (speculation, whole-stream
+    // SHA-1 mode), or compared with the grid digests
+    std::vector<uint64_t> sa;
+    std::vector<uint32_t> sl;
+    for (uint64_t i = 0; i < nk; ++i)
+      if (hk[i].pad == 2) sa.push_back(hk[i].p + 1 - W_);
+    std::vector<uint8_t> sh;
+    if (!sa.empty()) {
+      sh.resize(20 * sa.size());
       for (size_t off = 0; off < sa.size(); off += kFBatchMax) {
         const size_t m = std::min(sa.size() - off, kFBatchMax);
         const std::vector<uint64_t> pa(sa.begin() + off, sa.begin() + off + m);
-        const std::vector<uint32_t> pl(sl.begin() + off, sl.begin() + off + m);
-        const std::vector<uint8_t> sh = sha1s(pa, pl);
-        for (size_t j = 0; j < m; ++j) {
-          const uint64_t i = hidx[sidx[off + j]];
-          if (memcmp(&sh[20 * j], &c_.hsha[16 * (size_t)hc[i].ref], 16) == 0)
-            hcands_.push_back({hc[i].p, hc[i].ref});
-        }
+        sl.assign(m, W_);
+        const std::vector<uint8_t> part = sha1s(pa, sl);
+        memcpy(&sh[20 * off], part.data(), part.size());
       }
-      sort_by_position(hcands_);
     }
-    acands_.reserve(nc);
-    for (uint64_t i = 0; i < nc; ++i)
-      if (ok[i] && !hc[i].pad) acands_.push_back({hc[i].p, hc[i].ref});
-    sort_by_position(acands_);
+    hcands_.reserve(hcands_.size() + nk);
+    if (spec_) spec_hist_.reserve(spec_hist_.size() + nk);
+    size_t js = 0;
+    for (uint64_t i = 0; i < nk; ++i) {
+      const Cand& k = hk[i];
+      const uint8_t* pre = &c_.hsha[16 * (size_t)k.ref];
+      if (k.pad == 2) {
+        if (memcmp(&sh[20 * js++], pre, 16) == 0) hcands_.push_back({k.p, k.ref});
+        continue;
+      }
+      const uint64_t ws = k.p + 1 - W_;
+      if (spec_ && grid_sha_pending(ws)) {
+        hcands_.push_back({k.p, k.ref});
+        spec_hist_.push_back({wdiv(ws), k.ref});
+      } else if (const uint8_t* g = grid_sha_of(ws)) {
+        if (memcmp(g, pre, 16) == 0) hcands_.push_back({k.p, k.ref});
+      }
+    }
   }
 
   // LSD radix sort by window end (11-bit digits, stable).  Candidates with the
@@ -2301,6 +2406,7 @@ class Resolver {
       push(ws, W_, ZC_CHUNK_DUP, key);
       r_ = m + 1;
       s_ = r_;
+      const bool hist_match = m == ph && m != pg && m != pa && m != pf;
       if (lazy_) {
         // on the new grid: its chunk under the window is consumed; off it: the
         // grid moves again (back onto this epoch's grid: a real epoch)
@@ -2309,6 +2415,7 @@ class Resolver {
           if ((r_g_ - r_e_) % W_ == 0) return lazy_exit(r_ + W_ - 1);
         }
         x = r_ + W_ - 1;
+        if (hist_match) x = hist_run(ih, x, std::min(pa, pg), false);
         continue;
       }
       if ((r_ - r_e_) % W_ == 0) {
@@ -2321,6 +2428,7 @@ class Resolver {
         if (j >= ks_) ks_ = j + 1;
         if (m == pg) chain(j);
         x = r_ + W_ - 1;
+        if (hist_match) x = hist_run(ih, x, std::min(pa, pg), true);
         continue;
       }
       // grid shift: this epoch's grid ends at m; the walk goes on lazily
@@ -2329,6 +2437,50 @@ class Resolver {
       r_g_ = r_;
       x = r_ + W_ - 1;
     }
+  }
+
+  // After a historic match whose window ended at x - W (the walk now at x):
+  // the historic candidates that follow at x, x + W, x + 2W, ... -- an
+  // unchanged stretch of an earlier backup, found window after window -- are
+  // taken as one run of DUP records, written like the grid runs (in parallel
+  // when long, classified by finalize_records from the run alone).  Each is a
+  // match exactly where the walk stands (nothing can precede it: no flush
+  // piece, no other candidate before `bound`, no by-value key to screen), so
+  // the state after the run is what the walk would reach one match at a time:
+  // r = s = the run's end, and on this epoch's grid (same_grid) the grid
+  // chunks under the windows consumed.  Returns the walk's next position.
+  std::vector<uint64_t> run_keys_;
+  uint64_t hist_run(size_t& ih, uint64_t x, uint64_t bound, bool same_grid) {
+    if (has_f_) return x;
+    run_keys_.clear();
+    const uint64_t x0r = x;
+    size_t k = ih;
+    while (k < hcands_.size()) {
+      while (k < hcands_.size() && hcands_[k].p < x) ++k;  // (entries of a key chain at the window just taken)
+      if (k == hcands_.size() || hcands_[k].p != x || x >= h_end_ || x >= bound) break;
+      run_keys_.push_back(c_.hkey[hcands_[k].ref]);
+      x += W_;
+    }
+    const uint64_t nrun = run_keys_.size();
+    if (!nrun) return x0r;
+    ih = k;
+    const uint64_t ws0 = x0r - W_ + 1;
+    if (same_grid && indexable_) {
+      const uint64_t j0 = (ws0 - r_e_) / W_;
+      for (uint64_t j = j0; j < j0 + nrun && j < nspec_; ++j)
+        if (!dead_[nconf_ + j]) {
+          dead_[nconf_ + j] = 1;
+          ++ndead_;
+        }
+      if (j0 + nrun > ks_) ks_ = j0 + nrun;
+    }
+    const size_t o = c_.recs.size();
+    c_.recs.resize(o + nrun);
+    fill_grid_records(c_.recs.data() + o, nrun, ws0, 0, W_, ZC_CHUNK_DUP, run_keys_.data());
+    gruns_.push_back({o, nrun, ws0, (uint32_t)ZC_CHUNK_DUP});
+    r_ = x - W_ + 1;
+    s_ = r_;
+    return x;
   }
 
   // the grid chunks of this epoch saved by probe m become confirmed refs
@@ -2445,7 +2597,10 @@ class Resolver {
     struct Done {
       zc_stats& st;
       Clock::time_point t;
-      ~Done() { st.finalize_ms += ms_since(t); }
+      ~Done() {
+        st.finalize_ms += ms_since(t);
+        SpinTeam::disarm_any();  // the segment's parallel jobs are over
+      }
     } done{c_.stats, t0};
     std::vector<uint64_t> a, b;
     std::vector<size_t> rest;
@@ -2919,6 +3074,118 @@ int zc_seed_index(zc_ctx* c, const zc_seed* seeds, size_t n) {
   });
 }
 
+uint32_t zc_anchor_def(uint32_t chunk_max_size) { return chunk_max_size ? anchor_def_of(chunk_max_size) : 0u; }
+
+// ids with metadata join the historic index (key and SHA-1 prefix on the host,
+// first anchor / gear / fingerprint on the device, the anchor in its table),
+// the rest the by-value set: what ChunkIndex::loadIndex registers
+// (chunk_index.cc:26-79,163-182), split by how the engine can find each id
+int zc_seed_index_meta(zc_ctx* c, const zc_seed* seeds, size_t n, const zc_chunk_meta* meta, size_t nm) {
+  ZC_LOCK(c);
+  if (!c || (n && !seeds) || (nm && !meta)) return ZC_ERR_ARG;
+  if (c->nhist != c->nhist_seeded) {
+    c->err = "zc_seed_index_meta: the context's streams have added chunks to its index (seed before the first "
+             "stream, or after zc_forget_stream_chunks)";
+    return ZC_ERR_STATE;
+  }
+  return guarded(c, [&] {
+    DeviceGuard g(c->device);
+    const uint32_t W = c->W, def = anchor_def_of(W);
+    // usable metadata by rolling key (then SHA-1 prefix): W-byte chunks of
+    // this anchor definition with an anchor where a W-byte chunk can hold one
+    std::unordered_map<uint64_t, std::vector<uint32_t>> mk;
+    mk.reserve(nm);
+    for (size_t j = 0; j < nm; ++j) {
+      const zc_chunk_meta& m = meta[j];
+      if (m.size != W || m.anchor_def != def || m.anchor == ZC_NO_ANCHOR || m.anchor < ZC_ANCHOR_MIN_OFF ||
+          m.anchor >= W || W <= ZC_ANCHOR_MIN_OFF)
+        continue;
+      mk[m.rolling].push_back((uint32_t)j);
+    }
+    // historic ids already seeded, for registerNewChunkId's "unless present"
+    std::unordered_map<uint64_t, std::vector<uint32_t>> have;
+    for (uint32_t e = 0; e < c->nhist; ++e) have[c->hkey[e]].push_back(e);
+    const uint32_t e0 = c->nhist;
+    std::vector<uint32_t> anc, gv;
+    std::vector<uint64_t> fp;
+    for (size_t i = 0; i < n; ++i) {
+      const zc_seed& sd = seeds[i];
+      if (sd.size != W) continue;  // only W-byte entries can equal a W-byte window
+      const zc_chunk_meta* m = nullptr;
+      auto it = mk.find(sd.rolling);
+      if (it != mk.end())
+        for (uint32_t j : it->second)
+          if (memcmp(meta[j].sha1, sd.sha1, 16) == 0) {
+            m = &meta[j];
+            break;
+          }
+      if (!m) {
+        add_static_once(*c, sd.rolling, sd.sha1, 1);
+        continue;
+      }
+      auto& hv = have[sd.rolling];
+      bool dup = false;
+      for (uint32_t e : hv)
+        if (memcmp(&c->hsha[16 * (size_t)e], sd.sha1, 16) == 0) dup = true;
+      if (dup) continue;
+      const uint32_t e = e0 + (uint32_t)anc.size();
+      if (e == 0xFFFFFFFFu) throw ZcError{ZC_ERR_NOMEM, "historic index full"};
+      hv.push_back(e);
+      c->hkey.push_back(sd.rolling);
+      c->hsha.insert(c->hsha.end(), sd.sha1, sd.sha1 + 16);
+      anc.push_back(m->anchor);
+      gv.push_back(m->gear);
+      fp.push_back(m->fingerprint);
+    }
+    const uint32_t k = (uint32_t)anc.size();
+    if (!k) return;
+    c->hanc.grow_keep((uint64_t)e0 + k, e0, c->stream);
+    c->hg.grow_keep((uint64_t)e0 + k, e0, c->stream);
+    c->hfp.grow_keep((uint64_t)e0 + k, e0, c->stream);
+    c->hkey_d.grow_keep((uint64_t)e0 + k, e0, c->stream);
+    h2d(*c, c->hkey_d.p + e0, c->hkey.data() + e0, k);
+    h2d(*c, c->hanc.p + e0, anc.data(), k);
+    h2d(*c, c->hg.p + e0, gv.data(), k);
+    h2d(*c, c->hfp.p + e0, fp.data(), k);
+    c->nhist = e0 + k;
+    c->nhist_seeded = c->nhist;
+    hist_table(*c, e0);
+    sync(*c);  // (the host arrays above are freed on return)
+  });
+}
+
+int zc_export_chunk_meta(const zc_ctx* c, zc_chunk_meta* out, size_t cap, size_t* n_out) {
+  ZC_LOCK(c);
+  if (!c || !n_out || (cap && !out)) return ZC_ERR_ARG;
+  const uint32_t e0 = c->nhist_seeded, k = c->nhist - c->nhist_seeded;
+  *n_out = k;
+  if (k > cap) return ZC_ERR_ARG;
+  if (!k) return ZC_OK;
+  std::vector<uint32_t> anc(k), gv(k);
+  std::vector<uint64_t> fp(k);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(c->device) != hipSuccess) return ZC_ERR_HIP;
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(anc.data(), c->hanc.p + e0, k * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(gv.data(), c->hg.p + e0, k * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(fp.data(), c->hfp.p + e0, k * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (e != hipSuccess) return ZC_ERR_HIP;
+  const uint32_t def = anchor_def_of(c->W);
+  for (uint32_t i = 0; i < k; ++i) {
+    zc_chunk_meta& m = out[i];
+    memcpy(m.sha1, &c->hsha[16 * ((size_t)e0 + i)], 16);
+    m.rolling = c->hkey[e0 + i];
+    m.size = c->W;
+    m.anchor_def = def;
+    m.anchor = anc[i];
+    m.gear = anc[i] == ZC_NO_ANCHOR ? 0u : gv[i];
+    m.fingerprint = anc[i] == ZC_NO_ANCHOR ? 0ull : fp[i];
+  }
+  return ZC_OK;
+}
+
 int zc_set_window(zc_ctx* c, uint64_t bytes) {
   ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
@@ -3139,6 +3406,8 @@ int zc_get_stats(const zc_ctx* c, zc_stats* out) {
   *out = c->stats;
   out->hbm_bytes = ctx_hbm_bytes(*c);
   out->hist_entries = c->nhist;
+  out->hist_seeded = c->nhist_seeded;
+  out->by_value = c->statics.size();
   out->window_bytes = c->win_cap;
   return ZC_OK;
 }
@@ -3170,7 +3439,7 @@ int zc_forget_stream_chunks(zc_ctx* c) {
     c->statics.erase(std::remove_if(c->statics.begin(), c->statics.end(),
                                     [](const StaticEntry& e) { return !e.seeded; }),
                      c->statics.end());
-    index_truncate(*c, 0, c->statics.size(), true);
+    index_truncate(*c, c->nhist_seeded, c->statics.size(), true);
   });
 }
 

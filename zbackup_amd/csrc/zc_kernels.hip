@@ -1104,8 +1104,14 @@ __device__ __forceinline__ bool anc_missing(const uint32_t* __restrict__ anc_off
 // key, the ref and the fingerprint to compare (empty: all ones).
 constexpr uint64_t kEmpty = ~0ull;
 
-__device__ __forceinline__ uint32_t table_slot(uint32_t g, uint32_t tbits) {
-  return (uint32_t)(((uint64_t)g * kGolden) >> (64 - tbits));
+// The slot mixes the gear with the fingerprint: the gear alone has ~20 free
+// bits on random bytes but as few as 4 on content whose bytes of one parity
+// are constant (UTF-16 text: every odd byte 0, so st(q - 1) = 0 at every
+// anchor, and st(q) keeps only the 4 bits the anchor test leaves free), and
+// every chunk's anchor would then share 16 probe chains (quadratic inserts and
+// walks).  The 8 fingerprint bytes spread such keys like any others.
+__device__ __forceinline__ uint32_t table_slot(uint32_t g, uint64_t fp, uint32_t tbits) {
+  return (uint32_t)(((((uint64_t)g << 32) ^ fp) * kGolden) >> (64 - tbits));
 }
 
 // the probe's first level: bit (g mod 2^kGFiltBits) of every table key (the
@@ -1134,19 +1140,43 @@ struct EpochGrid {
   uint32_t nconf, nspec;
 };
 
-__device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
+// The probe's candidates are staged per wave in LDS and appended to the
+// global list with one atomic per wave (an incremental backup of unchanged
+// data emits a candidate per 64 KiB: 131,072 same-address atomics made the
+// probe 190 us per 8 GiB); a full stage spills to the global counter.
+constexpr uint32_t kCandStage = 128;
+struct CandOut {
+  Cand* cand;
+  uint64_t cap;
+  unsigned long long* counters;
+  Cand* stage;      // this wave's LDS stage
+  uint32_t* nstage; // its fill count (LDS)
+};
+__device__ __forceinline__ void emit_cand(const CandOut& co, uint64_t p, uint32_t ref, uint32_t pad) {
+  const uint32_t k = atomicAdd(co.nstage, 1u);
+  if (k < kCandStage) {
+    co.stage[k].p = p;
+    co.stage[k].ref = ref;
+    co.stage[k].pad = pad;
+    return;
+  }
+  const unsigned long long c = atomicAdd(&co.counters[CNT_CAND], 1ull);
+  if (c < co.cap) {
+    co.cand[c].p = p;
+    co.cand[c].ref = ref;
+    co.cand[c].pad = pad;
+  }
+}
+
+__device__ __forceinline__ void probe_anchor(uint64_t pos, uint32_t gk, uint64_t fp,
                                              const uint64_t* __restrict__ tab, uint32_t tbits,
                                              const uint32_t* __restrict__ anc_off, const uint32_t* __restrict__ cls,
                                              const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead,
                                              uint64_t r, uint64_t n, uint32_t W, const EpochGrid& eg,
-                                             Cand* __restrict__ cand, uint64_t cand_cap,
-                                             unsigned long long* __restrict__ counters) {
+                                             const CandOut& co) {
   if (pos < r + ZC_ANCHOR_MIN_OFF || !tab) return;
   const uint32_t mask = (1u << tbits) - 1;
-  uint32_t h = table_slot(gk, tbits);
-  // the filter passed, so the gear is almost surely in the table: the
-  // fingerprint loads go out together with the first slot's
-  const uint64_t fp = anchor_fp(data, pos);
+  uint32_t h = table_slot(gk, fp, tbits);
   for (;;) {
     const uint4 slot = *(const uint4*)(tab + 2 * (uint64_t)h);
     if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
@@ -1170,14 +1200,7 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
             const uint64_t j = (ws - eg.r_e) / W;
             grid_twin = j < eg.nspec && (eg.nconf + j == ref || cls[eg.nconf + j] == ref);
           }
-          if (p < n && p >= vr && !dr && !grid_twin) {
-            const unsigned long long c = atomicAdd(&counters[CNT_CAND], 1ull);
-            if (c < cand_cap) {
-              cand[c].p = p;
-              cand[c].ref = ref;
-              cand[c].pad = 0;
-            }
-          }
+          if (p < n && p >= vr && !dr && !grid_twin) emit_cand(co, p, ref, 0u);
         }
       }
     }
@@ -1190,14 +1213,11 @@ __device__ __forceinline__ void probe_anchor(const uint8_t* __restrict__ data, u
 // same layout.  Its entries are always visible and never consumed; a
 // candidate names the entry (pad = 1) and is confirmed by the window's key and
 // SHA-1 (chunk_index.cc:119-143), not by bytes.
-__device__ __forceinline__ void probe_hist(const uint8_t* __restrict__ data, uint64_t pos, uint32_t gk,
-                                           const HistTab& ht, uint64_t r, uint64_t n, uint32_t W,
-                                           Cand* __restrict__ cand, uint64_t cand_cap,
-                                           unsigned long long* __restrict__ counters) {
+__device__ __forceinline__ void probe_hist(uint64_t pos, uint32_t gk, uint64_t fp, const HistTab& ht, uint64_t r,
+                                           uint64_t n, uint32_t W, const CandOut& co) {
   if (pos < r + ZC_ANCHOR_MIN_OFF) return;
   const uint32_t mask = (1u << ht.bits) - 1;
-  uint32_t h = table_slot(gk, ht.bits);
-  const uint64_t fp = anchor_fp(data, pos);
+  uint32_t h = table_slot(gk, fp, ht.bits);
   for (;;) {
     const uint4 slot = *(const uint4*)(ht.tab + 2 * (uint64_t)h);
     if (slot.x == 0xFFFFFFFFu && slot.y == 0xFFFFFFFFu) break;  // empty
@@ -1206,14 +1226,7 @@ __device__ __forceinline__ void probe_hist(const uint8_t* __restrict__ data, uin
       const uint64_t o = ht.anc[e];
       if (pos >= r + o) {
         const uint64_t p = pos - o + W - 1;
-        if (p < n) {
-          const unsigned long long c = atomicAdd(&counters[CNT_CAND], 1ull);
-          if (c < cand_cap) {
-            cand[c].p = p;
-            cand[c].ref = e;
-            cand[c].pad = 1;
-          }
-        }
+        if (p < n) emit_cand(co, p, e, 1u);
       }
     }
     h = (h + 1) & mask;
@@ -1231,6 +1244,10 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
   const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   constexpr int kS = kProbeWT * kProbeSlots;
+  __shared__ Cand s_cand[kProbeTPB / 64][kCandStage];
+  __shared__ uint32_t s_ncand[kProbeTPB / 64];
+  const CandOut co{cand, cand_cap, counters, s_cand[threadIdx.x >> 6], &s_ncand[threadIdx.x >> 6]};
+  if (lane == 0) *co.nstage = 0;
   uint64_t wts[kProbeWT];
   TileAnchors ta[kProbeWT];
 #pragma unroll
@@ -1257,34 +1274,49 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     f[q] = live[q] && gfilt ? (gfilt[fb >> 5] >> (fb & 31)) & 1u : 0u;
     if (ht.tab) f[q] |= live[q] ? ((ht.filt[fb >> 5] >> (fb & 31)) & 1u) << 1 : 0u;
   }
-  // level 3: the offsets of the anchors that pass, compacted into the wave's
-  // LDS list {offset in the wave pair | wave-tile << 24, gear}
+  // level 3: the offsets of the anchors that pass; level 4: their
+  // fingerprints (the table slot mixes them in), every lane's in flight at
+  // once; both compacted into the wave's LDS lists {offset in the wave pair |
+  // wave-tile << 24, gear} and {fingerprint}
   __shared__ uint2 s_pass[kProbeTPB / 64][kS * 64];
+  __shared__ uint64_t s_fp[kProbeTPB / 64][kS * 64];
   uint2* const lst = s_pass[threadIdx.x >> 6];
+  uint64_t* const lfp = s_fp[threadIdx.x >> 6];
   uint32_t rel[kS];
 #pragma unroll
   for (int q = 0; q < kS; ++q) {
     const int t = q / kProbeSlots;
     rel[q] = f[q] ? ta[t].rel[lane + 64u * (q % kProbeSlots)] : 0u;
   }
+  // (anchors the walks skip -- before r + ZC_ANCHOR_MIN_OFF -- read nothing)
+  uint64_t fpv[kS];
+#pragma unroll
+  for (int q = 0; q < kS; ++q) {
+    const uint64_t pos = (wts[q / kProbeSlots] << ZC_WT_SHIFT) + rel[q];
+    fpv[q] = f[q] && pos >= r + ZC_ANCHOR_MIN_OFF ? anchor_fp(data, pos) : 0ull;
+  }
   static_assert(ZC_WT_SHIFT < 24 && kProbeWT <= 64, "pass-list packing");
   uint32_t np = 0;
 #pragma unroll
   for (int q = 0; q < kS; ++q) {
     const uint64_t m = __ballot(f[q] != 0u);
-    if (f[q]) lst[np + lane_prefix(m)] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24 | f[q] << 30, g[q]);
+    if (f[q]) {
+      const uint32_t at = np + lane_prefix(m);
+      lst[at] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24 | f[q] << 30, g[q]);
+      lfp[at] = fpv[q];
+    }
     np += (uint32_t)__popcll(m);
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // level 4: the table walks, one anchor per lane
+  // level 5: the table walks, one anchor per lane
   for (uint32_t j = lane; j < np; j += 64) {
     const uint2 a = lst[j];
+    const uint64_t fp = lfp[j];
     const uint32_t t = (a.x >> 24) & 63u;
     const uint64_t pos = ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu);
-    if (a.x & (1u << 30))
-      probe_anchor(data, pos, a.y, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, cand, cand_cap, counters);
-    if (a.x & (1u << 31)) probe_hist(data, pos, a.y, ht, r, n, W, cand, cand_cap, counters);
+    if (a.x & (1u << 30)) probe_anchor(pos, a.y, fp, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, co);
+    if (a.x & (1u << 31)) probe_hist(pos, a.y, fp, ht, r, n, W, co);
   }
   // wave-tiles with more anchors than the slots above
 #pragma unroll
@@ -1293,11 +1325,24 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
       const uint32_t gk = ta[t].g[e];
       const uint32_t fb = gk & ((1u << kGFiltBits) - 1);
       const uint64_t pos = (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e];
-      if (gfilt && ((gfilt[fb >> 5] >> (fb & 31)) & 1u))
-        probe_anchor(data, pos, gk, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, cand, cand_cap, counters);
-      if (ht.tab && ((ht.filt[fb >> 5] >> (fb & 31)) & 1u))
-        probe_hist(data, pos, gk, ht, r, n, W, cand, cand_cap, counters);
+      const bool pe = gfilt && ((gfilt[fb >> 5] >> (fb & 31)) & 1u);
+      const bool ph = ht.tab && ((ht.filt[fb >> 5] >> (fb & 31)) & 1u);
+      if ((!pe && !ph) || pos < r + ZC_ANCHOR_MIN_OFF) continue;
+      const uint64_t fp = anchor_fp(data, pos);
+      if (pe) probe_anchor(pos, gk, fp, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, co);
+      if (ph) probe_hist(pos, gk, fp, ht, r, n, W, co);
     }
+  }
+  // the wave's staged candidates: one atomic, then a lane per entry
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const uint32_t ns = min(*co.nstage, kCandStage);
+  if (ns) {
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&counters[CNT_CAND], (unsigned long long)ns);
+    base = __shfl(base, 0);
+    for (uint32_t k = lane; k < ns; k += 64)
+      if (base + k < cand_cap) cand[base + k] = co.stage[k];
   }
 }
 
@@ -1431,11 +1476,12 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
   atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
   const uint64_t word = ((uint64_t)i << 32) | g;
   const uint32_t mask = (1u << tbits) - 1;
-  for (uint32_t h = table_slot(g, tbits);; h = (h + 1) & mask) {
+  const uint64_t fpi = cfp[i];
+  for (uint32_t h = table_slot(g, fpi, tbits);; h = (h + 1) & mask) {
     const unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
                                               (unsigned long long)word);
     if (prev == kEmpty) {
-      tab[2 * (uint64_t)h + 1] = cfp[i];
+      tab[2 * (uint64_t)h + 1] = fpi;
       return;
     }
   }
@@ -1455,11 +1501,12 @@ __global__ void zc_hist_insert_kernel(const uint32_t* __restrict__ g, const uint
   atomicOr(&filt[fb >> 5], 1u << (fb & 31));
   const uint64_t word = ((uint64_t)e << 32) | gv;
   const uint32_t mask = (1u << bits) - 1;
-  for (uint32_t h = table_slot(gv, bits);; h = (h + 1) & mask) {
+  const uint64_t fpe = fp[e];
+  for (uint32_t h = table_slot(gv, fpe, bits);; h = (h + 1) & mask) {
     const unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
                                               (unsigned long long)word);
     if (prev == kEmpty) {
-      tab[2 * (uint64_t)h + 1] = fp[e];
+      tab[2 * (uint64_t)h + 1] = fpe;
       return;
     }
   }
@@ -1554,6 +1601,166 @@ __global__ void __launch_bounds__(256) zc_class_verify_kernel(
     }
   }
   if (lane == 0 && joined) atomicAdd(&counters[CNT_CLASS], joined);
+}
+
+// ---------------------------------------------------------------------------
+// The probe's candidates, checked and ordered on the device (the host walk
+// needs the historic ones key-checked and in position order; checking 131,072
+// of them one by one on the host and radix-sorting them took 2.8 ms of an
+// incremental 8 GiB backup).  Four launches:
+//   zc_cand_split: thread per candidate.  An epoch candidate (pad 0: bytes to
+//     verify against its ref) is appended to out0.  A historic one (pad 1) is
+//     kept iff its window's rolling key equals the entry's -- findChunk's first
+//     test (chunk_index.cc:119-143; the SHA-1 prefix, its second, stays with the
+//     host, which holds the prefixes) -- and takes a rank in its position
+//     bucket p >> bshift (rank ~0: dropped).
+//   zc_bucket_scan: the buckets' exclusive prefix sum (one workgroup).
+//   zc_cand_scatter: each kept candidate to its bucket's slots, flagged 1 when
+//     its window is a grid chunk whose SHA-1 the side stream computes (joined
+//     by key now, its prefix checked when the digests land), else 2 (the host
+//     hashes the window).
+//   zc_bucket_sort: thread per bucket, its few entries by position; a bucket of
+//     more than kBucketSortMax (pathological: many entries sharing an anchor
+//     and its offset) is left unsorted and flagged, and the host sorts the list.
+constexpr uint32_t kBucketSortMax = 64;
+enum { HC_EPOCH = 0, HC_KEPT = 1, HC_UNSORTED = 2, HC_EPOCH_OUT = 3, HC_LAST = 4 };
+
+__global__ void zc_cand_split_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk,
+                                     const Cand* __restrict__ cand, uint32_t nc, const uint64_t* __restrict__ hkey,
+                                     uint64_t pw, uint32_t W, uint32_t bshift, uint32_t* __restrict__ rank,
+                                     uint32_t* __restrict__ bcnt, Cand* __restrict__ out0,
+                                     unsigned long long* __restrict__ hc) {
+  ZC_URGENT();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  const Cand c = cand[i];
+  uint32_t rk = ~0u;
+  if (c.pad == 0) {
+    out0[atomicAdd(&hc[HC_EPOCH], 1ull)] = c;
+  } else if (pw + rk_acc(data, blk, c.p + 1 - W, c.p + 1) == hkey[c.ref]) {
+    rk = atomicAdd(&bcnt[c.p >> bshift], 1u);
+  }
+  rank[i] = rk;
+}
+
+// exclusive prefix sum of cnt[0, nb) into off[0, nb], off[nb] = the total
+// (also hc[HC_KEPT]), in three coalesced launches: block sums of 1024 buckets
+// (256 threads x 4), their scan (one workgroup), each block's own scan plus
+// its offset.  (One workgroup walking the counts with a contiguous share per
+// thread took 0.70 ms beside the grid SHA-1: every load a scattered line on
+// one CU.)  The scan launch also moves the epoch-candidate count hc[HC_EPOCH]
+// to hc[HC_EPOCH_OUT] and clears hc[HC_EPOCH] and hc[HC_UNSORTED] for the next
+// call, so hc needs no fill between calls.
+constexpr uint32_t kScanItems = 4, kScanTPB = 256, kScanBlockItems = kScanItems * kScanTPB;
+
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) lds[w] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t k = 0; k < w; ++k) before += lds[k];
+  total = lds[0] + lds[1] + lds[2] + lds[3];
+  __syncthreads();
+  return before + x - v;
+}
+
+__device__ __forceinline__ void load4_cnt(const uint32_t* __restrict__ cnt, uint32_t nb, uint32_t i0, uint32_t* v) {
+#pragma unroll
+  for (uint32_t k = 0; k < kScanItems; ++k) v[k] = i0 + k < nb ? cnt[i0 + k] : 0u;
+}
+
+__global__ void __launch_bounds__(kScanTPB) zc_bucket_sums_kernel(const uint32_t* __restrict__ cnt, uint32_t nb,
+                                                                  uint32_t* __restrict__ bsum) {
+  ZC_URGENT();
+  __shared__ uint32_t lds[4];
+  uint32_t v[kScanItems];
+  load4_cnt(cnt, nb, blockIdx.x * kScanBlockItems + threadIdx.x * kScanItems, v);
+  uint32_t total;
+  (void)block_excl_scan256(v[0] + v[1] + v[2] + v[3], lds, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// the block sums' exclusive scan in place (nblk <= kScanBlockItems: one pass)
+__global__ void __launch_bounds__(kScanTPB) zc_bucket_bscan_kernel(uint32_t* __restrict__ bsum, uint32_t nblk,
+                                                                   uint32_t* __restrict__ off, uint32_t nb,
+                                                                   unsigned long long* __restrict__ hc) {
+  ZC_URGENT();
+  __shared__ uint32_t lds[4];
+  uint32_t v[kScanItems];
+  const uint32_t i0 = threadIdx.x * kScanItems;
+  load4_cnt(bsum, nblk, i0, v);
+  uint32_t total;
+  uint32_t run = block_excl_scan256(v[0] + v[1] + v[2] + v[3], lds, total);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanItems; ++k) {
+    if (i0 + k < nblk) bsum[i0 + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) {
+    off[nb] = total;
+    hc[HC_KEPT] = total;
+    hc[HC_EPOCH_OUT] = hc[HC_EPOCH];
+    hc[HC_EPOCH] = 0;
+    hc[HC_UNSORTED] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(kScanTPB) zc_bucket_offsets_kernel(const uint32_t* __restrict__ cnt, uint32_t nb,
+                                                                     const uint32_t* __restrict__ bsum,
+                                                                     uint32_t* __restrict__ off) {
+  ZC_URGENT();
+  __shared__ uint32_t lds[4];
+  uint32_t v[kScanItems];
+  const uint32_t i0 = blockIdx.x * kScanBlockItems + threadIdx.x * kScanItems;
+  load4_cnt(cnt, nb, i0, v);
+  uint32_t total;
+  uint32_t run = bsum[blockIdx.x] + block_excl_scan256(v[0] + v[1] + v[2] + v[3], lds, total);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanItems; ++k) {
+    if (i0 + k < nb) off[i0 + k] = run;
+    run += v[k];
+  }
+}
+
+__global__ void zc_cand_scatter_kernel(const Cand* __restrict__ cand, uint32_t nc, const uint32_t* __restrict__ rank,
+                                       const uint32_t* __restrict__ off, uint32_t bshift, uint64_t n_gsha, uint32_t W,
+                                       uint64_t n, Cand* __restrict__ out) {
+  ZC_URGENT();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  const uint32_t rk = rank[i];
+  if (rk == ~0u) return;
+  Cand c = cand[i];
+  const uint64_t ws = c.p + 1 - W;
+  const bool grid = n_gsha && ws % W == 0 && ws / W < n_gsha && ws + W <= n;
+  c.pad = grid ? 1u : 2u;
+  out[off[c.p >> bshift] + rk] = c;
+}
+
+__global__ void zc_bucket_sort_kernel(Cand* __restrict__ out, const uint32_t* __restrict__ off, uint32_t nb,
+                                      uint32_t* __restrict__ bcnt, unsigned long long* __restrict__ hc) {
+  ZC_URGENT();
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  bcnt[b] = 0;  // zero again for the next call (the buffer is zeroed once, when made)
+  const uint32_t lo = off[b], hi = off[b + 1];
+  if (hi - lo < 2) return;
+  if (hi - lo > kBucketSortMax) {
+    atomicMax(&hc[HC_UNSORTED], 1ull);
+    return;
+  }
+  for (uint32_t i = lo + 1; i < hi; ++i) {
+    const Cand x = out[i];
+    uint32_t j = i;
+    for (; j > lo && out[j - 1].p > x.p; --j) out[j] = out[j - 1];
+    out[j] = x;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2444,7 +2651,7 @@ __global__ void __launch_bounds__(64) zc_key64_filter_kernel(const uint8_t* __re
     }
   key64_trim(runs, i, r, first, last);
 }
-__global__ void __launch_bounds__(64) zc_key64_filter_wave_kernel(const uint8_t* __restrict__ data,
+__global__ void __launch_bounds__(256) zc_key64_filter_wave_kernel(const uint8_t* __restrict__ data,
                                                                   const uint64_t* __restrict__ blk, uint32_t W,
                                                                   uint64_t pw, Run* __restrict__ runs, uint64_t nruns,
                                                                   const uint64_t* __restrict__ set, uint32_t sbits,
@@ -2452,18 +2659,21 @@ __global__ void __launch_bounds__(64) zc_key64_filter_wave_kernel(const uint8_t*
                                                                   uint32_t nl) {
   ZC_URGENT();
   static_assert(kKey64FilterMax <= 64, "a lane per position");
-  const uint64_t i = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  if (i >= nruns) return;
-  const Run r = runs[i];
-  if (r.end - r.start <= kKey64LaneMax || r.end - r.start > kKey64FilterMax) return;
-  const uint64_t p = r.start + lane;
-  bool hit = false;
-  if (p < r.end) hit = key64_in(pw + rk_acc(data, blk, p + 1 - W, p + 1), set, sbits, zero_key, list, nl);
-  const uint64_t m = __ballot(hit);
-  if (lane == 0)
-    key64_trim(runs, i, r, m ? r.start + (uint64_t)__builtin_ctzll(m) : ~0ull,
-               m ? r.start + 63 - (uint64_t)__builtin_clzll(m) : 0);
+  // a bounded grid of waves strides over the runs (most are short and left to
+  // zc_key64_filter_kernel: a wave skips them after one load)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < nruns; i += nw) {
+    const Run r = runs[i];
+    if (r.end - r.start <= kKey64LaneMax || r.end - r.start > kKey64FilterMax) continue;
+    const uint64_t p = r.start + lane;
+    bool hit = false;
+    if (p < r.end) hit = key64_in(pw + rk_acc(data, blk, p + 1 - W, p + 1), set, sbits, zero_key, list, nl);
+    const uint64_t m = __ballot(hit);
+    if (lane == 0)
+      key64_trim(runs, i, r, m ? r.start + (uint64_t)__builtin_ctzll(m) : ~0ull,
+                 m ? r.start + 63 - (uint64_t)__builtin_clzll(m) : 0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2864,6 +3074,43 @@ hipError_t launch_range_digest_small(const uint8_t* data, uint64_t n, const uint
   return hipGetLastError();
 }
 
+// the results to the host's pinned buffers in one pass (the runtime's
+// device-to-host blits ran beside the grid SHA-1 at its priority: 27 us for
+// the 32-byte counters, 129 us for 2 MB): the lists, 16-byte stores, then the
+// counters (system-scope stores; the host reads them after the stream syncs)
+__global__ void zc_cand_out_kernel(const Cand* __restrict__ out0, const Cand* __restrict__ out,
+                                   const unsigned long long* __restrict__ hc, Cand* __restrict__ h_out0,
+                                   Cand* __restrict__ h_out, unsigned long long* __restrict__ h_hc) {
+  ZC_URGENT();
+  const uint64_t n0 = hc[HC_EPOCH_OUT], nk = hc[HC_KEPT];
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n0 + nk; i += gs) {
+    if (i < nk) h_out[i] = out[i];
+    else h_out0[i - nk] = out0[i - nk];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < HC_LAST) h_hc[threadIdx.x] = hc[threadIdx.x];
+}
+
+hipError_t launch_cand_order(const uint8_t* data, const uint64_t* blk, const Cand* cand, uint32_t nc,
+                             const uint64_t* hkey, uint64_t pw, uint32_t W, uint64_t n, uint64_t n_gsha,
+                             CandOrderBufs b, hipStream_t s) {
+  if (!nc) return hipSuccess;
+  const uint32_t nblk = (uint32_t)blocks_for(b.nb, kScanBlockItems);
+  if (nblk > kScanBlockItems) return hipErrorInvalidValue;  // (nb <= 2^20 by the caller's bucket size)
+  hipLaunchKernelGGL(zc_cand_split_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, data, blk, cand, nc, hkey, pw, W,
+                     b.bshift, b.rank, b.bcnt, b.out0, b.hc);
+  hipLaunchKernelGGL(zc_bucket_sums_kernel, dim3(nblk), dim3(kScanTPB), 0, s, b.bcnt, b.nb, b.bsum);
+  hipLaunchKernelGGL(zc_bucket_bscan_kernel, dim3(1), dim3(kScanTPB), 0, s, b.bsum, nblk, b.boff, b.nb, b.hc);
+  hipLaunchKernelGGL(zc_bucket_offsets_kernel, dim3(nblk), dim3(kScanTPB), 0, s, b.bcnt, b.nb, b.bsum, b.boff);
+  hipLaunchKernelGGL(zc_cand_scatter_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, cand, nc, b.rank, b.boff,
+                     b.bshift, n_gsha, W, n, b.out);
+  hipLaunchKernelGGL(zc_bucket_sort_kernel, dim3(blocks_for(b.nb, 256)), dim3(256), 0, s, b.out, b.boff, b.nb, b.bcnt,
+                     b.hc);
+  hipLaunchKernelGGL(zc_cand_out_kernel, dim3(std::min<unsigned>(blocks_for(nc, 256), 1024)), dim3(256), 0, s, b.out0,
+                     b.out, b.hc, b.h_out0, b.h_out, b.h_hc);
+  return hipGetLastError();
+}
+
 hipError_t launch_range_digest(const uint8_t* data, uint64_t n, const uint64_t* blk, const uint64_t* a,
                                const uint64_t* b, uint32_t nr, uint64_t* out, hipStream_t s) {
   if (!nr) return hipSuccess;
@@ -3007,10 +3254,13 @@ hipError_t launch_key64_filter(const uint8_t* data, const uint64_t* blk, uint32_
                                uint64_t nruns, const uint64_t* set, uint32_t sbits, int zero_key,
                                const uint64_t* list, uint32_t nl, hipStream_t s) {
   if (!nruns) return hipSuccess;
-  if (nruns > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  // a launch's work-items must stay below 2^32: 64-thread blocks, one lane per run
+  if (nruns >= (1ull << 32) - 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(zc_key64_filter_kernel, dim3(blocks_for(nruns, 64)), dim3(64), 0, s, data, blk, W, pw, runs,
                      nruns, set, sbits, zero_key, list, nl);
-  hipLaunchKernelGGL(zc_key64_filter_wave_kernel, dim3((unsigned)nruns), dim3(64), 0, s, data, blk, W, pw, runs,
+  // one wave per run, at most 4096 workgroups of 4 waves striding over them
+  const uint64_t wblocks = std::min<uint64_t>((nruns + 3) / 4, 4096);
+  hipLaunchKernelGGL(zc_key64_filter_wave_kernel, dim3((unsigned)wblocks), dim3(256), 0, s, data, blk, W, pw, runs,
                      nruns, set, sbits, zero_key, list, nl);
   return hipGetLastError();
 }
