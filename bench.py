@@ -153,15 +153,48 @@ def launch(argv, world, script=None, extra_env=None):
 
 # --------------------------------------------------------------------------
 
-def cpu_baseline(sample_bytes, seed):
-    """The oracle port (per-byte rotate + identity-hash hash_map probe + SHA-1
-    per chunk, single thread) on the first `sample_bytes` of the same stream."""
+def cpu_sample_bytes(sample_bytes, seed, config):
+    """The first `sample_bytes` of the config's stream, on the host: C2 random;
+    C3 a random block and its copy (sample_bytes / 2 each, the duplicated shape
+    at sample scale); C5 zeros."""
+    import numpy as np
     from oracle import oracle
-    data = oracle.splitmix64(sample_bytes, seed)
+    if config == "c5":
+        return np.zeros(sample_bytes, dtype=np.uint8)
+    if config == "c3":
+        half = oracle.splitmix64(sample_bytes // 2, seed)
+        return np.concatenate([half, half])
+    return oracle.splitmix64(sample_bytes, seed)
+
+
+def cpu_baseline(sample_bytes, seed, config="c2"):
+    """The oracle port (per-byte rotate + identity-hash hash_map probe + SHA-1
+    per chunk, single thread) on a sample of the same stream."""
+    from oracle import oracle
+    data = cpu_sample_bytes(sample_bytes, seed, config)
     t0 = time.perf_counter()
     recs = oracle.chunk(data, W64)
     dt = time.perf_counter() - t0
     return {"value": sample_bytes / dt / 2**30, "seconds": dt, "records": len(recs)}
+
+
+def host_cpu():
+    """The host CPU this process runs on: model name, logical CPUs the machine
+    has and the ones this process may use (read at run time, on the GPU box)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
 
 
 def committed_profile(build_id):
@@ -768,7 +801,15 @@ def run_rank(args):
                "sample": f"first {args.cpu_sample_mib} MiB of each rank's C2 stream (seed {args.seed}+rank), "
                          f"oracle/zc_oracle.cpp single thread per rank, {world} concurrent; rank 0: "
                          f"{c['records']} records in {c['seconds']:.2f} s",
-               "per_process": [round(v, 5) for v in per]}
+               "per_process": [round(v, 5) for v in per], "host": host_cpu()}
+        if world == 1 and not args.no_extras:
+            # the other single-GPU configs' shapes at sample scale
+            for cfg in ("c3", "c5"):
+                co = cpu_baseline(args.cpu_sample_mib << 20, seed, cfg)
+                cpu[f"value_{cfg}"] = {"value": round(co["value"], 5), "unit": "GiB/s", "cores": 1,
+                                       "sample": f"{args.cpu_sample_mib} MiB of the {cfg.upper()} shape "
+                                                 f"({CONFIGS[cfg]}), {co['records']} records in "
+                                                 f"{co['seconds']:.2f} s"}
 
     if rank == 0:
         from zbackup_amd import _lib
@@ -804,11 +845,21 @@ def run_rank(args):
             "stages": stage_dict(st),
         }
         if rp_ms and args.config == "c2" and n == 8 << 30:
-            # the same kernel's average under rocprofv3 (committed summary)
+            # the headline fraction is the committed rocprofv3 --kernel-trace
+            # --stats average of THIS build's scan (the profile is keyed on the
+            # build id); this run's own HIP-event average stays beside it as
+            # events_frac (it is another box's clock)
+            out["roofline"]["events_achieved"] = out["roofline"]["achieved"]
+            out["roofline"]["events_frac"] = out["roofline"]["frac"]
+            out["roofline"]["achieved"] = round(n / (rp_ms * 1e-3) / 1e9, 1)
+            out["roofline"]["frac"] = round(n / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            out["roofline"]["frac_source"] = "rocprof"
             out["roofline"]["rocprof"] = {"scan_ms_avg": round(rp_ms, 4),
                                           "achieved": round(n / (rp_ms * 1e-3) / 1e9, 1),
                                           "frac": round(n / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                           "source": rp_src}
+        else:
+            out["roofline"]["frac_source"] = "events (no committed rocprof profile of this build)"
         if prof is None:
             out["roofline"]["profile"] = f"no committed profiles/rNN_scan_profile.json of build {build_id}"
         else:

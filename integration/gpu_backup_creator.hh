@@ -5,10 +5,13 @@
 // backup_creator.cc.  ZBackup::backupFromFileHandle (zutils.cc:89-182) keeps its
 // read loop and its iterative shrink loop; it only constructs these classes:
 //
-//   GpuChunkIndex gpuIndex( config, chunkIndex, 0 );            // once per backup
+//   GpuChunkIndex gpuIndex( config, chunkIndex, 0, ZC_FLAG_SHA1, metaDir );  // once per backup
 //   GpuBackupCreator backupCreator( gpuIndex, chunkStorageWriter );  // zutils.cc:96
 //   ...
 //   GpuBackupCreator backupCreator( gpuIndex, chunkStorageWriter );  // zutils.cc:140
+//   ...
+//   chunkStorageWriter.commit();                                     // zutils.cc:175
+//   gpuIndex.saveChunkMeta( metaDir );   // metaDir = Dir::addPath( dir, "zchunk" )
 //
 // GpuChunkIndex is the device-side probe set: one libzchunk context, seeded
 // with every chunk id of the repository's index files (ChunkIndex::loadIndex
@@ -26,9 +29,13 @@
 #ifndef GPU_BACKUP_CREATOR_HH_INCLUDED
 #define GPU_BACKUP_CREATOR_HH_INCLUDED
 
+#include <dirent.h>
 #include <google/protobuf/io/zero_copy_stream_impl_lite.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <mutex>
 #include <stdexcept>
@@ -51,6 +58,123 @@ inline void zcCheck( int rc, zc_ctx * ctx, char const * what )
     throw std::runtime_error( std::string( what ) + ": " + ( ctx ? zc_last_error( ctx ) : "libzchunk" ) );
 }
 
+/// The content-anchor metadata of a repository's chunks (zc_chunk_meta, ABI 5),
+/// kept in files of its own beside the index -- "<repo>/zchunk/<sha256 hex>" --
+/// and never inside index/ or bundles/, whose formats stay zbackup's.  One
+/// file per backup, written at the end of the backup next to the index file
+/// Writer::commit moves into place (chunk_storage.cc:61-90); a new process
+/// reads every file and seeds the ids ChunkIndex::loadIndex reports together
+/// with the entries that match them by full ChunkId.  The metadata is a pure
+/// function of a chunk's bytes, so it never goes stale: entries of chunks a gc
+/// removed are simply never joined to an id, and a file that is damaged or of
+/// another anchor definition only costs speed (those ids are screened by key),
+/// never a different backup.
+///
+/// File: "ZCMETA01", LE32 record size (48), LE32 0, LE64 count, count records,
+/// then the SHA-256 of everything before it (zc_sha256_*); written to a
+/// temporary name and renamed, as tmp_mgr.cc:16-24 does for zbackup's files.
+class GpuChunkMetaSidecar
+{
+  static void sha256( std::string const & data, unsigned char out[ 32 ] )
+  {
+    zc_sha256 * h = 0;
+    if ( zc_sha256_create( &h ) != ZC_OK )
+      throw std::runtime_error( "zc_sha256_create" );
+    zc_sha256_add( h, data.data(), data.size() );
+    zc_sha256_finish( h, out );
+    zc_sha256_destroy( h );
+  }
+
+public:
+  /// the entries of one file; false (and nothing added) if it is not a valid one
+  static bool read( std::string const & path, std::vector< zc_chunk_meta > & out )
+  {
+    FILE * f = fopen( path.c_str(), "rb" );
+    if ( !f )
+      return false;
+    std::string data;
+    char buf[ 65536 ];
+    size_t rd;
+    while ( ( rd = fread( buf, 1, sizeof( buf ), f ) ) > 0 )
+      data.append( buf, rd );
+    fclose( f );
+    if ( data.size() < 24 + 32 || data.compare( 0, 8, "ZCMETA01" ) != 0 )
+      return false;
+    uint32_t recSize;
+    uint64_t count;
+    memcpy( &recSize, data.data() + 8, 4 );
+    memcpy( &count, data.data() + 16, 8 );
+    if ( recSize != sizeof( zc_chunk_meta ) || count > ( data.size() - 56 ) / recSize ||
+         data.size() != 24 + count * recSize + 32 )
+      return false;
+    unsigned char want[ 32 ];
+    sha256( data.substr( 0, data.size() - 32 ), want );
+    if ( memcmp( want, data.data() + data.size() - 32, 32 ) != 0 )
+      return false;
+    size_t at = out.size();
+    out.resize( at + count );
+    memcpy( &out[ at ], data.data() + 24, count * recSize );
+    return true;
+  }
+
+  /// every valid file of dir (a missing dir: none)
+  static void readDir( std::string const & dir, std::vector< zc_chunk_meta > & out )
+  {
+    DIR * d = opendir( dir.c_str() );
+    if ( !d )
+      return;
+    while ( struct dirent * e = readdir( d ) )
+    {
+      std::string name( e->d_name );
+      if ( name.size() == 64 && name.find_first_not_of( "0123456789abcdef" ) == std::string::npos )
+        read( dir + "/" + name, out );
+    }
+    closedir( d );
+  }
+
+  /// the metadata of the chunks ctx's streams added, as one new file of dir
+  /// (made if missing); returns its path, or "" when there is nothing to write
+  static std::string write( std::string const & dir, zc_ctx * ctx )
+  {
+    size_t n = 0;
+    zc_export_chunk_meta( ctx, 0, 0, &n );
+    if ( !n )
+      return std::string();
+    std::vector< zc_chunk_meta > meta( n );
+    zcCheck( zc_export_chunk_meta( ctx, meta.data(), meta.size(), &n ), ctx, "zc_export_chunk_meta" );
+    std::string data( "ZCMETA01", 8 );
+    uint32_t words[ 2 ] = { (uint32_t)sizeof( zc_chunk_meta ), 0 };
+    uint64_t count = n;
+    data.append( (char const *)words, 8 );
+    data.append( (char const *)&count, 8 );
+    data.append( (char const *)meta.data(), n * sizeof( zc_chunk_meta ) );
+    unsigned char sum[ 32 ];
+    sha256( data, sum );
+    data.append( (char const *)sum, 32 );
+    char hex[ 65 ];
+    for ( int i = 0; i < 32; ++i )
+      snprintf( hex + 2 * i, 3, "%02x", sum[ i ] );
+    mkdir( dir.c_str(), 0755 );
+    std::string path = dir + "/" + hex, tmp = path + ".tmp";
+    FILE * f = fopen( tmp.c_str(), "wb" );
+    if ( !f || fwrite( data.data(), 1, data.size(), f ) != data.size() || fflush( f ) != 0 ||
+         fsync( fileno( f ) ) != 0 )
+    {
+      if ( f )
+        fclose( f );
+      unlink( tmp.c_str() );
+      throw std::runtime_error( "chunk metadata: cannot write " + tmp );
+    }
+    fclose( f );
+    if ( rename( tmp.c_str(), path.c_str() ) != 0 )
+    {
+      unlink( tmp.c_str() );
+      throw std::runtime_error( "chunk metadata: cannot rename " + tmp );
+    }
+    return path;
+  }
+};
+
 /// The repository's chunk index on the GPU (one libzchunk context)
 class GpuChunkIndex: NoCopy, public IndexProcessor
 {
@@ -59,17 +183,31 @@ class GpuChunkIndex: NoCopy, public IndexProcessor
 
 public:
   /// flags: ZC_FLAG_SHA1 (the default) is what zbackup needs -- the instruction
-  /// stream carries whole ChunkIds (backup_creator.cc:127-141,231-234)
-  GpuChunkIndex( Config const & config, ChunkIndex & chunkIndex, int device, uint32_t flags = ZC_FLAG_SHA1 ):
+  /// stream carries whole ChunkIds (backup_creator.cc:127-141,231-234).
+  /// metaDir: the repository's chunk-metadata directory (GpuChunkMetaSidecar),
+  /// or "" to seed the ids alone
+  GpuChunkIndex( Config const & config, ChunkIndex & chunkIndex, int device, uint32_t flags = ZC_FLAG_SHA1,
+                 std::string const & metaDir = std::string() ):
     ctx( 0 )
   {
     zcCheck( zc_create( &ctx, config.GET_STORABLE( chunk, max_size ), device, flags ), 0, "zc_create" );
     chunkIndex.loadIndex( *this );  // every chunk id of every index file -> processChunk
-    zcCheck( zc_seed_index( ctx, seeds.data(), seeds.size() ), ctx, "zc_seed_index" );
+    std::vector< zc_chunk_meta > meta;
+    if ( !metaDir.empty() )
+      GpuChunkMetaSidecar::readDir( metaDir, meta );
+    if ( meta.empty() )
+      zcCheck( zc_seed_index( ctx, seeds.data(), seeds.size() ), ctx, "zc_seed_index" );
+    else
+      zcCheck( zc_seed_index_meta( ctx, seeds.data(), seeds.size(), meta.data(), meta.size() ), ctx,
+               "zc_seed_index_meta" );
     std::vector< zc_seed >().swap( seeds );
   }
   ~GpuChunkIndex() { zc_destroy( ctx ); }
   zc_ctx * context() { return ctx; }
+
+  /// after chunkStorageWriter.commit() (zutils.cc:175): the metadata of the
+  /// chunks this backup wrote, as a new file of metaDir
+  std::string saveChunkMeta( std::string const & metaDir ) { return GpuChunkMetaSidecar::write( metaDir, ctx ); }
 
   // IndexProcessor (chunk_index.hh:47-55)
   void startIndex( string const & ) {}

@@ -3,10 +3,13 @@
 // getInputBuffer / handleMoreData, finish, then the iterative shrink passes on
 // the same index -- over the stand-in types of tests/adapter/mock.
 //
-//   adapter_main W input seeds.bin|- out_prefix
+//   adapter_main W input seeds.bin|- out_prefix [meta_dir]
 //     seeds.bin: zc_seed records (the repository's index before the backup)
+//     meta_dir: the repository's chunk-metadata directory (GpuChunkMetaSidecar):
+//       read when the index is seeded, a file for this backup written at its end
 //     writes out_prefix.data (the final backup data), out_prefix.meta
-//     ("iterations adds"), out_prefix.adds (24-byte ids of Writer::add calls)
+//     ("iterations adds hist_seeded by_value"), out_prefix.adds (24-byte ids of
+//     Writer::add calls)
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -15,10 +18,11 @@
 #include "gpu_backup_creator.hh"
 
 int main(int argc, char** argv) {
-  if (argc != 5) {
-    fprintf(stderr, "usage: %s W input seeds.bin|- out_prefix\n", argv[0]);
+  if (argc != 5 && argc != 6) {
+    fprintf(stderr, "usage: %s W input seeds.bin|- out_prefix [meta_dir]\n", argv[0]);
     return 2;
   }
+  const std::string metaDir = argc == 6 ? argv[5] : "";
   StorableConfig st;
   st.chunk_.max_size_ = (uint32_t)strtoul(argv[1], 0, 10);
   Config config;
@@ -38,7 +42,9 @@ int main(int argc, char** argv) {
   }
   ChunkStorage::Writer chunkStorageWriter;
   try {
-    GpuChunkIndex gpuIndex(config, chunkIndex, 0);
+    GpuChunkIndex gpuIndex(config, chunkIndex, 0, ZC_FLAG_SHA1, metaDir);
+    zc_stats seeded;
+    zcCheck(zc_get_stats(gpuIndex.context(), &seeded), gpuIndex.context(), "zc_get_stats");
     FILE* in = fopen(argv[2], "rb");
     if (!in) return 3;
     GpuBackupCreator backupCreator(gpuIndex, chunkStorageWriter);
@@ -76,6 +82,9 @@ int main(int argc, char** argv) {
         break;
       }
     }
+    // Writer::commit (zutils.cc:175) would move the bundles and the index file
+    // into place here; the chunk metadata of this backup follows it
+    if (!metaDir.empty()) gpuIndex.saveChunkMeta(metaDir);
     const std::string p(argv[4]);
     FILE* f = fopen((p + ".data").c_str(), "wb");
     fwrite(serialized.data(), 1, serialized.size(), f);
@@ -84,7 +93,8 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < chunkStorageWriter.ids.size(); ++i) fwrite(chunkStorageWriter.ids[i].data(), 1, 24, f);
     fclose(f);
     f = fopen((p + ".meta").c_str(), "w");
-    fprintf(f, "%u %zu\n", iterations, chunkStorageWriter.ids.size());
+    fprintf(f, "%u %zu %llu %llu\n", iterations, chunkStorageWriter.ids.size(),
+            (unsigned long long)seeded.hist_seeded, (unsigned long long)seeded.by_value);
     fclose(f);
   } catch (const std::exception& e) {
     fprintf(stderr, "adapter_main: %s\n", e.what());
