@@ -304,7 +304,7 @@ def timed_steps(torch, world, step, warmup, steps, min_warmup_s=MIN_WARMUP_S):
     return job_elapsed(time.perf_counter() - t0, world), scan
 
 
-def static_leg(torch, buf, local, ks=(300000, 2000000), nbytes=1 << 30, reps=3):
+def static_leg(torch, buf, local, ks=(300000, 2000000, 8000000), nbytes=1 << 30, reps=3):
     """The static index at repository scale: the first GiB of
     the stream against K random ids known by value only (ChunkIndex::loadIndex
     of earlier backups' index files, chunk_index.cc:26-79), rolling-hash ids;
@@ -312,7 +312,8 @@ def static_leg(torch, buf, local, ks=(300000, 2000000), nbytes=1 << 30, reps=3):
     import numpy as np
     from zbackup_amd import BackupCreator
     out = {"unit": "GiB/s", "stream_bytes": nbytes, "chunk_max_size": W64,
-           "note": "two-level Bloom screen below 384 K ids, one-level with the in-kernel check table above (DESIGN 4.3)"}
+           "note": "two-level Bloom screen below 384 K ids, one-level with the in-kernel check table above (DESIGN 4.3); "
+                   "8 M ids: a 512 GiB repository at W = 64 KiB"}
     for k in ks:
         rng = np.random.default_rng(k)
         keys = rng.integers(1, 2**63, k, dtype=np.int64).astype(np.uint64)
@@ -544,6 +545,10 @@ def feed_bench(n, seed, sha1, copy_threads=8, sha256=2):
     eng = d["engine_and_adapter_s"]
     return {"value": round(n / d["loop_s"] / 2**30, 3), "unit": "GiB/s",
             "engine_and_adapter_GiB_per_s": round(n / eng / 2**30, 3) if eng > 0 else None,
+            "engine_and_adapter_note": "loop minus the input copies, Writer::add's payload appends, the SHA-256 and "
+                                      "the feed window's one-time setup (window_setup_s: pinning its host mirror)",
+            "window_setup_s": d.get("window_setup_s"), "segments": d.get("segments"),
+            "engine_resolve_ms": d.get("engine_total_ms"),
             "loop_s": d["loop_s"], "copy_s": d["copy_s"], "copy_threads": d["copy_threads"],
             "writer_add_s": d["writer_add_s"], "engine_and_adapter_s": eng, "shrink_s": d["shrink_s"],
             "shrink_iterations": d["shrink_iterations"], "writer_chunks": d["writer_chunks"],

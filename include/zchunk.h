@@ -184,6 +184,9 @@ uint32_t zc_anchor_def(uint32_t chunk_max_size);
  * The payload bytes of records taken (NEW chunks for Writer::add, BYTES for
  * bytes_to_emit) stay readable with zc_read_stream until the next
  * zc_get_input_buffer / zc_get_input_buffer_size / zc_feed / zc_finish call. */
+/* (the window's buffers are made on a helper thread from this call on, joined
+ * by the first zc_get_input_buffer: call it early -- before the index load --
+ * to overlap the ~0.3 s it takes to pin 1 GiB of host memory) */
 int zc_set_window(zc_ctx* ctx, uint64_t bytes);
 uint64_t zc_get_window(const zc_ctx* ctx);
 void* zc_get_input_buffer(zc_ctx* ctx);

@@ -122,20 +122,37 @@ RECORD_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u4"), ("kind", "<u4"),
 OPT_PREFILTER = 1
 
 
+SEED_DTYPE = np.dtype([("sha1", np.uint8, 16), ("rolling", "<u8"), ("size", "<u4"), ("pad", "<u4")])
+
+
+def seed_array(seeds):
+    """Seeds as a SEED_DTYPE array (laid out like Seed): a list of (sha1_16,
+    rolling, size) tuples, or such an array already (passed through)."""
+    if isinstance(seeds, np.ndarray):
+        return np.ascontiguousarray(seeds, dtype=SEED_DTYPE)
+    seeds = list(seeds)
+    out = np.zeros(len(seeds), dtype=SEED_DTYPE)
+    if seeds:
+        out["sha1"] = np.frombuffer(b"".join(bytes(sha16)[:16] for sha16, _, _ in seeds),
+                                    dtype=np.uint8).reshape(-1, 16)
+        out["rolling"] = np.array([rolling for _, rolling, _ in seeds], dtype=np.uint64)
+        out["size"] = np.array([size for _, _, size in seeds], dtype=np.uint32)
+    return out
+
+
 def chunk_array(data, W, seeds=(), prefilter=True):
     """The same run as chunk(), returned as a numpy structured array laid out
     like zc_record (for full-size comparisons).  prefilter=True puts an exact
-    key bitmap in front of the hash_map: identical records, faster misses."""
+    key bitmap in front of the hash_map: identical records, faster misses.
+    seeds: (sha1_16, rolling, size) tuples or a SEED_DTYPE array."""
     L = lib()
     data = np.ascontiguousarray(data, dtype=np.uint8)
-    seed_arr = (Seed * max(len(seeds), 1))()
-    for i, (sha16, rolling, size) in enumerate(seeds):
-        seed_arr[i].sha1[:] = list(sha16)
-        seed_arr[i].rolling = rolling
-        seed_arr[i].size = size
+    sa = seed_array(seeds)
+    assert SEED_DTYPE.itemsize == ctypes.sizeof(Seed)
+    seed_arr = (Seed * max(len(sa), 1)).from_buffer(sa) if len(sa) else (Seed * 1)()
     out = ctypes.POINTER(Record)()
     nout = ctypes.c_size_t()
-    rc = L.zco_chunk_ex(data.ctypes.data, data.size, W, seed_arr, len(seeds), 0,
+    rc = L.zco_chunk_ex(data.ctypes.data, data.size, W, seed_arr, len(sa), 0,
                         OPT_PREFILTER if prefilter else 0, ctypes.byref(out), ctypes.byref(nout))
     if rc:
         raise RuntimeError(f"zco_chunk_ex failed: {rc}")

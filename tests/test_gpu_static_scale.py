@@ -75,6 +75,30 @@ def test_large_static_index_device_vs_oracle(torch_cuda, nrand):
         _same(bc.records(), want)
 
 
+@pytest.mark.parametrize("nrand", [4000000])
+def test_static_index_4m_ids_device_vs_oracle(torch_cuda, nrand):
+    # 4 M random ids (a 256 GiB repository at W = 64 KiB) plus the stream's own:
+    # the one-level screen with its check table at 4 M keys, every record vs
+    # the oracle seeded with the same ids (as arrays: no per-id Python objects)
+    from zbackup_amd import BackupCreator
+    real, _ = _seeds(0)
+    rng = np.random.default_rng(nrand)
+    sa = np.zeros(nrand, dtype=oracle.SEED_DTYPE)
+    sa["rolling"] = rng.integers(1, 2**63, nrand, dtype=np.int64).astype(np.uint64)
+    sa["sha1"] = rng.integers(0, 256, (nrand, 16), dtype=np.uint8)
+    sa["size"] = W64
+    seeds = np.concatenate([oracle.seed_array(real), sa])
+    data = oracle.gen(SPEC)
+    want = oracle.chunk_array(data, W64, seeds=seeds)
+    assert (want["kind"] == 1).sum() >= len(real) - 1
+    t = torch_cuda.from_numpy(data).to("cuda")
+    with BackupCreator(W64, sha1=True) as bc:
+        bc.seed_index_arrays(seeds["sha1"], seeds["rolling"], seeds["size"])
+        assert bc.stats()["by_value"] == len(seeds)
+        bc.chunk_device(t.data_ptr(), data.size)
+        _same(bc.records(), want)
+
+
 @pytest.mark.parametrize("nrand", [300000, 1000000])
 def test_large_static_index_window_vs_oracle(torch_cuda, nrand):
     from zbackup_amd import BackupCreator

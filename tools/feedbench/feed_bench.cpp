@@ -14,7 +14,7 @@
 // before the next getInputBuffer (the piece's bytes are overwritten then);
 // 0 leaves it out.
 //
-//   feed_bench W bytes seed sha1(0|1) copy_threads [sha256(0|1|2)]
+//   feed_bench W bytes seed sha1(0|1) copy_threads [sha256(0|1|2) [window_bytes]]
 // prints one JSON object: seconds of the whole loop and of its parts
 #include <stdio.h>
 #include <stdlib.h>
@@ -64,11 +64,12 @@ void copy_mt(void* dst, const void* src, size_t n, unsigned threads) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc != 6 && argc != 7) {
-    fprintf(stderr, "usage: %s W bytes seed sha1 copy_threads [sha256]\n", argv[0]);
+  if (argc < 6 || argc > 8) {
+    fprintf(stderr, "usage: %s W bytes seed sha1 copy_threads [sha256 [window_bytes]]\n", argv[0]);
     return 2;
   }
-  const int sha256_mode = argc == 7 ? atoi(argv[6]) : 0;
+  const int sha256_mode = argc >= 7 ? atoi(argv[6]) : 0;
+  const uint64_t window = argc == 8 ? strtoull(argv[7], 0, 0) : 0;  // 0: the library's default
   const uint32_t W = (uint32_t)strtoul(argv[1], 0, 10);
   const uint64_t n = strtoull(argv[2], 0, 0), seed = strtoull(argv[3], 0, 0);
   const bool sha1 = atoi(argv[4]) != 0;
@@ -82,8 +83,9 @@ int main(int argc, char** argv) {
   ChunkIndex chunkIndex;
   ChunkStorage::Writer writer;
   try {
-    GpuChunkIndex gpuIndex(config, chunkIndex, 0, sha1 ? ZC_FLAG_SHA1 : 0);
-    double copy_s = 0, sha256_s = 0;
+    GpuChunkIndex gpuIndex(config, chunkIndex, 0, (sha1 ? ZC_FLAG_SHA1 : 0) | ZC_FLAG_TIMING);
+    if (window && zc_set_window(gpuIndex.context(), window) != ZC_OK) throw std::runtime_error("zc_set_window");
+    double copy_s = 0, sha256_s = 0, getbuf_s = 0, hmd_s = 0, window_setup_s = 0;
     size_t pieces = 0;
     zc_sha256* sha256 = nullptr;
     if (sha256_mode && zc_sha256_create(&sha256) != ZC_OK) throw std::runtime_error("zc_sha256_create");
@@ -97,8 +99,12 @@ int main(int argc, char** argv) {
         hasher.join();
         sha256_s += since(tj);
       }
+      const auto tg = Clock::now();
       size_t toRead = backupCreator.getInputBufferSize();
       void* inputBuffer = backupCreator.getInputBuffer();
+      // the first call makes the context's feed window (pinned host mirror +
+      // HBM: a per-context setup cost, reported apart); later ones slide it
+      (pieces ? getbuf_s : window_setup_s) += since(tg);
       const size_t rd = (size_t)std::min<uint64_t>(toRead, n - pos);
       if (!rd) break;
       const auto tc = Clock::now();
@@ -113,9 +119,15 @@ int main(int argc, char** argv) {
       } else if (sha256_mode == 2) {
         hasher = std::thread([=] { zc_sha256_add(sha256, inputBuffer, rd); });
       }
+      const auto thm = Clock::now();
       backupCreator.handleMoreData((unsigned)rd);
+      hmd_s += since(thm);
     }
+    const auto tf = Clock::now();
     backupCreator.finish();
+    const double finish_s = since(tf);
+    zc_stats stats;  // the backup stream's (the shrink passes are streams of their own)
+    zc_get_stats(gpuIndex.context(), &stats);
     std::string sha256_hex;
     if (sha256) {
       uint8_t dg[32];
@@ -155,16 +167,18 @@ int main(int argc, char** argv) {
       }
     }
     const double shrink_s = since(ts);
-    zc_stats stats;
-    zc_get_stats(gpuIndex.context(), &stats);
     printf("{\"bytes\": %llu, \"W\": %u, \"sha1\": %d, \"copy_threads\": %u, \"pieces\": %zu, \"loop_s\": %.6f, "
            "\"copy_s\": %.6f, \"writer_add_s\": %.6f, \"engine_and_adapter_s\": %.6f, \"shrink_s\": %.6f, "
            "\"shrink_iterations\": %u, \"writer_chunks\": %zu, \"writer_bytes\": %zu, \"bundles\": %zu, "
            "\"backup_data_bytes\": %zu, \"window_bytes\": %llu, \"sha256_mode\": %d, \"sha256_s\": %.6f, "
-           "\"sha256\": \"%s\"}\n",
+           "\"sha256\": \"%s\", \"window_setup_s\": %.6f, \"getbuf_s\": %.6f, \"handle_more_data_s\": %.6f, \"finish_s\": %.6f, "
+           "\"segments\": %llu, \"engine_total_ms\": %.3f, \"engine_meta_ms\": %.3f, \"engine_walk_ms\": %.3f, "
+           "\"engine_finalize_ms\": %.3f, \"engine_scan_ms\": %.3f}\n",
            (unsigned long long)n, W, sha1 ? 1 : 0, threads, pieces, loop_s, copy_s, writer.seconds,
-           loop_s - copy_s - writer.seconds - sha256_s, shrink_s, iterations, writer.chunks, writer.bytes, writer.bundles + 1,
-           serialized.size(), (unsigned long long)stats.window_bytes, sha256_mode, sha256_s, sha256_hex.c_str());
+           loop_s - copy_s - writer.seconds - sha256_s - window_setup_s, shrink_s, iterations, writer.chunks, writer.bytes, writer.bundles + 1,
+           serialized.size(), (unsigned long long)stats.window_bytes, sha256_mode, sha256_s, sha256_hex.c_str(),
+           window_setup_s, getbuf_s, hmd_s, finish_s, (unsigned long long)stats.segments, stats.total_ms, stats.meta_ms,
+           stats.walk_ms, stats.finalize_ms, stats.scan_ms);
   } catch (const std::exception& e) {
     fprintf(stderr, "feed_bench: %s\n", e.what());
     return 1;

@@ -387,6 +387,11 @@ struct zc_ctx {
   uint64_t win_cap = 0;
   DevBuf<uint8_t> dwin;
   HostBuf<uint8_t> hwin;
+  // the window's buffers made on a helper thread (zc_set_window), joined by
+  // window_open: pinning 1 GiB of host memory takes ~0.3 s, which a caller can
+  // overlap with its index load (ChunkIndex::loadIndex) this way
+  std::thread win_alloc;
+  std::string win_alloc_err;
   uint64_t wbase = 0, wend = 0;
   bool slide_pending = false;  // a segment was resolved: slide before the next input
   bool windowed_last = false;  // the last stream came through the window
@@ -2905,8 +2910,36 @@ uint64_t window_for(uint64_t want, uint32_t W) {
   return (m + ZC_STILE - 1) / ZC_STILE * ZC_STILE;
 }
 
+void window_alloc_join(zc_ctx& c) {
+  if (!c.win_alloc.joinable()) return;
+  c.win_alloc.join();
+  if (!c.win_alloc_err.empty()) {
+    std::string e;
+    e.swap(c.win_alloc_err);
+    throw ZcError{ZC_ERR_NOMEM, "feed window: " + e};
+  }
+}
+
+// start making the window's buffers on a helper thread
+void window_alloc_start(zc_ctx& c) {
+  window_alloc_join(c);
+  if (!c.win_cap || (c.dwin.cap >= c.win_cap && c.hwin.cap >= c.win_cap && c.dwin.p && c.hwin.p)) return;
+  c.win_alloc = std::thread([&c] {
+    try {
+      DeviceGuard g(c.device);
+      c.dwin.ensure(c.win_cap);
+      c.hwin.ensure(c.win_cap);
+    } catch (const ZcError& e) {
+      c.win_alloc_err = e.msg;
+    } catch (const std::exception& e) {
+      c.win_alloc_err = e.what();
+    }
+  });
+}
+
 void window_open(zc_ctx& c) {
   if (c.res) return;
+  window_alloc_join(c);
   c.dwin.ensure(c.win_cap);
   c.hwin.ensure(c.win_cap);
   c.wbase = c.wend = 0;
@@ -3043,6 +3076,7 @@ int zc_destroy(zc_ctx* c) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->win_alloc.joinable()) c->win_alloc.join();
     window_close(*c);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -3190,8 +3224,11 @@ int zc_set_window(zc_ctx* c, uint64_t bytes) {
   ZC_LOCK(c);
   if (!c) return ZC_ERR_ARG;
   if (c->res || c->n_stream) return ZC_ERR_STATE;
-  c->win_cap = bytes ? window_for(bytes, c->W) : 0;
-  return ZC_OK;
+  return guarded(c, [&] {
+    window_alloc_join(*c);
+    c->win_cap = bytes ? window_for(bytes, c->W) : 0;
+    window_alloc_start(*c);  // (joined by the first getInputBuffer)
+  });
 }
 
 uint64_t zc_get_window(const zc_ctx* c) { return c ? c->win_cap : 0; }
@@ -3403,6 +3440,7 @@ int zc_take_records(zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
 int zc_get_stats(const zc_ctx* c, zc_stats* out) {
   ZC_LOCK(c);
   if (!c || !out) return ZC_ERR_ARG;
+  if (c->win_alloc.joinable()) const_cast<zc_ctx*>(c)->win_alloc.join();  // (its error stays for window_open)
   *out = c->stats;
   out->hbm_bytes = ctx_hbm_bytes(*c);
   out->hist_entries = c->nhist;

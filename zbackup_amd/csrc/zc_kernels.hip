@@ -188,23 +188,27 @@ __device__ __forceinline__ uint32_t load4_any(const uint8_t* base, uint64_t addr
 // ---------------------------------------------------------------------------
 // zc_scan (the HBM-bound pass)
 //
-// Persistent workgroups of 512 lanes (8 waves, one workgroup per CU, two
-// waves per SIMD); each lane owns a 4 KiB span, a tile is 512 spans = 2 MiB.
-// Every wave streams its own 64 rows through a private 2-slot LDS ring of
-// 128-byte rounds with global_load_lds_dwordx4; the round after the current
-// one is always in flight, and the ring continues across the workgroup's
-// tiles.  One DMA instruction fills 8 rows x 128 B (whole cache lines); the
-// LDS image is linear and the global source is swizzled (piece p of row i sits
-// at piece p ^ ((i >> 1) & 7)), so the per-lane ds_read_b128 of a row is
-// bank-conflict free (MI355X_MICROARCH.md §LDS lane groups).  Round -1 of a
-// tile stages the bytes before each span (gear warm-up).  Waves never touch
-// each other's LDS: no barriers.  (tools/ubench/stage_bench.hip measured this
-// staging shape at 5.5 TB/s with no per-byte work.)
+// Persistent workgroups of 4 waves (one per SIMD), two workgroups per CU (two
+// waves per SIMD); each lane owns a 4 KiB span, a wave's 64 spans are a
+// 256 KiB wave-tile, and every wave walks wave-tiles on its own (2 MiB tiles of
+// 8 wave-tiles remain the unit of launch_scan_tiles).  Every wave streams its
+// own 64 rows through a private ONE-slot LDS ring of 128-byte rounds with
+// buffer_load ... lds (non-temporal): a round is read out of the slot, the slot
+// is refilled with the next round, then the round is hashed, so one round is
+// in flight per wave while it computes.  One DMA instruction fills 8 rows x
+// 128 B (whole cache lines); the LDS image is linear and the global source is
+// swizzled (piece p of row i sits at piece p ^ ((i >> 1) & 7)), so the per-lane
+// ds_read_b128 of a row is bank-conflict free (MI355X_MICROARCH.md §LDS lane
+// groups); odd lanes take the two halves of their span in the other order (a
+// row stride of 4 KiB alone cost the staging 12 %).  The 32 bytes before each
+// half span (the anchor state's warm-up) are two register loads issued with
+// the DMA of the half's first round.  Waves never touch each other's LDS: no
+// barriers.  (DESIGN 4.1 has the measured geometry experiments 1-22.)
 //
-// Anchors are appended to a per-wave LDS list (one ballot per dword on the
-// fast path; a wave-uniform block in the ~22 % of dwords where any lane hits)
-// and moved to the per-span global slots once per tile, so no global store is
-// outstanding while the ring is being waited on.
+// Anchors are appended to a per-wave LDS list (one ballot per 16-byte piece; a
+// wave-uniform block in the ~22 % of pieces where any lane hits) and moved to
+// the wave-tile's pool share once per wave-tile, in position order, with their
+// store instructions counted so the next round's wait leaves them in flight.
 struct ScanLane {
   uint32_t glo;       // anchor state {st(q - 1), st(q)} after position q (zc_device.h)
   uint32_t hlo, hhi;  // 64-bit Rabin-Karp accumulator of the current 1 KiB span
