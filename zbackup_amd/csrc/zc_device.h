@@ -276,6 +276,9 @@ struct EpochIndex {
   const uint8_t* gsha;  // null: every pair by bytes
   uint64_t n_gsha;
   uint64_t* hkey = nullptr;  // pinned host copy of the grid chunks' keys (key + nconf), or null
+  // the scan's counters (2) to hand to the host (pinned h_scnt) and clear, or null
+  unsigned long long* scnt = nullptr;
+  unsigned long long* h_scnt = nullptr;
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,

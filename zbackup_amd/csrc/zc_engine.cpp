@@ -155,6 +155,52 @@ struct HostBuf {
   const T& operator[](size_t i) const { return p[i]; }
 };
 
+// A growable array of trivially copyable records whose capacity beyond its
+// size is plain memory the owner may write ahead into (an epoch's grid records
+// are written while the device batch runs, and adopted by the walk's resize).
+template <class T>
+class RecordVec {
+ public:
+  RecordVec() = default;
+  RecordVec(const RecordVec&) = delete;
+  RecordVec& operator=(const RecordVec&) = delete;
+  ~RecordVec() { free(p_); }
+  size_t size() const { return n_; }
+  size_t capacity() const { return cap_; }
+  bool empty() const { return n_ == 0; }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  void clear() { n_ = 0; }
+  void reserve(size_t c) {
+    if (c > cap_) grow(c);
+  }
+  void resize(size_t n) {  // new elements keep whatever the memory holds
+    if (n > cap_) grow(std::max(n, 2 * cap_));
+    n_ = n;
+  }
+  void push_back(const T& v) {
+    if (n_ == cap_) grow(std::max<size_t>(64, 2 * cap_));
+    p_[n_++] = v;
+  }
+  void erase_front(size_t k) {  // drop the first k elements
+    k = std::min(k, n_);
+    if (k < n_) memmove(p_, p_ + k, (n_ - k) * sizeof(T));
+    n_ -= k;
+  }
+
+ private:
+  void grow(size_t c) {
+    T* q = (T*)realloc(p_, c * sizeof(T));
+    if (!q) throw std::bad_alloc();
+    p_ = q;
+    cap_ = c;
+  }
+  T* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+};
+
 struct StaticEntry {
   uint64_t key;
   uint8_t sha[16];
@@ -371,6 +417,7 @@ struct zc_ctx {
   hipStream_t sha_stream = nullptr;   // SHA-1 of the grid chunks, beside the scan (ZC_FLAG_SHA1)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   hipEvent_t ev_sha = nullptr;  // the grid chunks' SHA-1 (sha_stream) are complete
+  hipEvent_t ev_grec = nullptr;  // an epoch's chunk metadata is in: its grid records can be written
   std::string err;
 
   // host feed
@@ -435,7 +482,7 @@ struct zc_ctx {
   // filled in) and not yet taken (zc_take_records); records past nrec_done are
   // being cut.  The taken prefix is dropped once it is most of the vector, so
   // draining a long stream in small batches stays linear.
-  std::vector<zc_record, DefaultInit<zc_record>> recs;  // resize leaves new records to be written
+  RecordVec<zc_record> recs;  // resize leaves new records to be written; grid records may be written ahead
   // the resolver's per-stream lists, kept here for their capacity (Resolver):
   // a list built fresh per stream is new pages, and an incremental backup's
   // candidate lists are megabytes
@@ -478,6 +525,11 @@ struct zc_ctx {
   DevBuf<uint32_t> prel, pg, srel, sg;  // anchor pool and side pool
   DevBuf<uint32_t> otiles, obase;
   DevBuf<unsigned long long> counters;
+  // the scan's own two counters (anchors pooled, wave-tiles overflowed), zero
+  // between scans: the first epoch's chunk-metadata kernel hands them to
+  // h_scnt and clears them (no copy behind the scan, no fill before the next)
+  DevBuf<unsigned long long> scnt;
+  bool scnt_dirty = true;  // unknown contents (new, or a stream that failed): clear first
   DevBuf<uint8_t> gsha;  // SHA-1 of the first epoch's grid chunks (ZC_FLAG_SHA1)
   HostBuf<uint2> h_pairs;  // an epoch's pairs of grid chunks joined by speculation
   HostBuf<uint8_t> h_gsha;  // ... copied back on the SHA-1 stream right behind the kernel
@@ -529,7 +581,38 @@ template <class T>
 void d2h(zc_ctx& c, T* dst, const T* src, size_t n) {
   if (n) HCK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyDeviceToHost, c.stream));
 }
-void sync(zc_ctx& c) { HCK(hipStreamSynchronize(c.stream)); }
+// Waits for a stream by polling it: a blocking wait returned 10-20 us after
+// the work had ended (its wake-up), and the epoch's batch is waited for on
+// every stream's critical path.  Past kSpinMaxMs it blocks.
+constexpr double kSpinMaxMs = 4.0;
+void wait_stream(hipStream_t s) {
+  const auto t0 = Clock::now();
+  for (unsigned i = 1;; ++i) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HCK(e);
+    if ((i & 255) == 0 && ms_since(t0) > kSpinMaxMs) {
+      HCK(hipStreamSynchronize(s));
+      return;
+    }
+    _mm_pause();
+  }
+}
+void sync(zc_ctx& c) { wait_stream(c.stream); }
+// the same for an event
+void wait_event(hipEvent_t ev) {
+  const auto t0 = Clock::now();
+  for (unsigned i = 1;; ++i) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HCK(e);
+    if ((i & 255) == 0 && ms_since(t0) > kSpinMaxMs) {
+      HCK(hipEventSynchronize(ev));
+      return;
+    }
+    _mm_pause();
+  }
+}
 
 // ---------------------------------------------------------------------------
 // the context's index beyond the stream being resolved
@@ -710,7 +793,10 @@ class Resolver {
   // reading the caller's buffer, which the caller may free once the call
   // has returned its error.
   ~Resolver() {
-    if (std::uncaught_exceptions() > 0) drain();
+    if (std::uncaught_exceptions() > 0) {
+      drain();
+      c_.scnt_dirty = true;  // a scan's counters may not have been handed over
+    }
   }
   void drain() {
     (void)hipStreamSynchronize(c_.sha_stream);
@@ -762,8 +848,8 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
-      scan_counters_clear();
-      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.counters.p,
+      scnt_pending_ = true;
+      HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.scnt.p,
                             c_.stream));
       tiles_done_ = t1;
     }
@@ -803,8 +889,8 @@ class Resolver {
         if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
         scan_open_ = true;
       }
-      scan_counters_clear();
-      HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.counters.p, c_.stream));
+      scnt_pending_ = true;
+      HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.scnt.p, c_.stream));
       if (!windowed_) pre_sha();
       scan_finish();
       lim_ = n_;
@@ -1174,9 +1260,17 @@ class Resolver {
     c_.pg.ensure(nwt * wcap_);
     c_.srel.ensure(1);
     c_.sg.ensure(1);
-    c_.counters.ensure(CNT_LAST);
+    if (!c_.counters.p) {  // (every user clears what it counts in; zeroed once when made)
+      c_.counters.ensure(CNT_LAST);
+      HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+    }
     c_.h_cnt.ensure(CNT_LAST);
-    HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+    c_.scnt.ensure(2);
+    c_.h_scnt.ensure(CNT_LAST);
+    if (c_.scnt_dirty) {
+      HCK(hipMemsetAsync(c_.scnt.p, 0, 2 * sizeof(unsigned long long), c_.stream));
+      c_.scnt_dirty = false;
+    }
   }
 
   // The scan's counters are read back with the first epoch's batch (no
@@ -1193,9 +1287,15 @@ class Resolver {
       if (!(c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_idx, c_.stream));
       side_wait_ = (c_.flags & ZC_FLAG_TIMING) ? c_.ev1 : c_.ev_idx;
     }
-    c_.h_scnt.ensure(CNT_LAST);
-    d2h(c_, c_.h_scnt.p, c_.counters.p, CNT_LAST);
     scan_checked_ = false;
+  }
+  // the scan's counters to h_scnt (and cleared) unless the next batch's
+  // chunk-metadata kernel does it; the caller synchronises before reading
+  void scan_counters_readback() {
+    if (!scnt_pending_) return;
+    scnt_pending_ = false;
+    d2h(c_, c_.h_scnt.p, c_.scnt.p, 2);
+    HCK(hipMemsetAsync(c_.scnt.p, 0, 2 * sizeof(unsigned long long), c_.stream));
   }
 
   // after a synchronisation that covers the scan: anchor count, scan timing,
@@ -1203,6 +1303,10 @@ class Resolver {
   // (work queued on the provisional pool must be redone)
   bool scan_check() {
     if (scan_checked_) return false;
+    if (scnt_pending_) {  // no batch took the scan's counters: read them now
+      scan_counters_readback();
+      sync(c_);
+    }
     scan_checked_ = true;
     if ((c_.flags & ZC_FLAG_TIMING) && scan_open_) {
       float ms = 0;
@@ -1215,10 +1319,7 @@ class Resolver {
     const uint64_t found = c_.h_scnt[CNT_POOL];
     npool_ += found;
     c_.stats.anchors += found;
-    // the next scan launch counts from zero (cleared right before it, if one
-    // comes: a fill queued here ran beside the grid SHA-1 at its priority and
-    // held up the epoch's own device work by ~25 us)
-    scan_counters_dirty_ = true;
+    // (the next scan launch counts from zero: the hand-off cleared them)
     if (c_.h_scnt[CNT_OVERFLOW] && wt_hi > wt_lo) {
       // wave-tiles whose anchors overflowed the scan's LDS list or their pool
       // share (dense data): count them exactly, then rescan into a side pool
@@ -1257,12 +1358,7 @@ class Resolver {
     return false;
   }
   bool scan_checked_ = true;
-  bool scan_counters_dirty_ = false;
-  void scan_counters_clear() {
-    if (!scan_counters_dirty_) return;
-    scan_counters_dirty_ = false;
-    HCK(hipMemsetAsync(c_.counters.p, 0, 2 * sizeof(unsigned long long), c_.stream));
-  }
+  bool scnt_pending_ = false;  // scans queued whose counters are still on the device
   bool meta_from_scan_ = false;  // ev1 marks the end of scan launches queued for this batch
   hipEvent_t side_wait_ = nullptr;  // the copy stream's next work waits for this scan end
 
@@ -1278,6 +1374,7 @@ class Resolver {
     c_.stats.epochs++;
     r_e_ = s_;
     ks_ = 0;
+    grec_ = grec_valid_ = false;
     const uint64_t xs = x0();
     h_end_ = hspan_ ? std::min<uint64_t>(lim_, xs + hspan_) : lim_;
     // grid chunks cut in the rotate phase (the last W bytes are the ring at
@@ -1349,13 +1446,22 @@ class Resolver {
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
                         pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_, nsref ? c_.h_key.p : nullptr};
-        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream));
+        if (scnt_pending_) {  // the chunk-metadata kernel hands the scan's counters over
+          ix.scnt = c_.scnt.p;
+          ix.h_scnt = c_.h_scnt.p;
+          scnt_pending_ = false;
+        }
+        grec_valid_ = false;
+        grec_ = !windowed_ && indexable_ && nsref >= kGridRecordsMin;
+        HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream,
+                               grec_ ? c_.ev_grec : nullptr));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
         dev_nspec_ = nsref;
         dev_valid_ = true;
       } else {
         HCK(hipMemsetAsync(c_.counters.p, 0, CNT_LAST * sizeof(unsigned long long), c_.stream));
+        scan_counters_readback();
       }
       const uint64_t* tab = nref_ && anchors ? c_.tab.p : nullptr;
       // ZC_FLAG_SHA1, speculative (spec_): equal-key grid pairs are joined
@@ -1383,8 +1489,24 @@ class Resolver {
       // the grid SHA-1 behind the batch's read-back too: that copy runs alone
       // (beside the SHA-1 it took 14 us instead of 6), the SHA-1 a few us later
       sha_launch();
+      // While the rest of the batch runs, the host writes the epoch's grid
+      // records ahead, past the end of the record array, as the walk will
+      // when no match comes first (it then adopts them): they need only the
+      // grid keys, which the chunk-metadata kernel stores into pinned memory.
+      // (Written by the device instead -- a kernel beside the batch storing
+      // 5 MB into pinned memory -- they took 109 us of PCIe writes and slowed
+      // the index insert from 23 to 119 us; the host has this time idle.)
+      if (grec_) {
+        const size_t o_e = c_.recs.size();
+        c_.recs.reserve(o_e + nsref + 64);
+        wait_event(c_.ev_grec);
+        fill_grid_records(c_.recs.data() + o_e, nsref, r_e_, 0, W_, ZC_CHUNK_NEW, c_.h_key.p);
+        grec_valid_ = true;
+        grec_o_ = o_e;
+        grec_n_ = nsref;
+      }
       sync(c_);
-      HCK(hipStreamSynchronize(c_.copy_stream));
+      wait_stream(c_.copy_stream);
       if (scan_check()) {  // the pool changed under this epoch: queue it again
         c_.stats.epochs--;
         return true;
@@ -2229,6 +2351,14 @@ class Resolver {
     }
   }
 
+  // the grid records of this epoch written ahead (epoch()): grid chunk k's
+  // record at index grec_o_ + k, k < grec_n_
+  static constexpr uint32_t kGridRecordsMin = 16384;
+  bool grec_ = false;  // this epoch's grid records are written ahead
+  bool grec_valid_ = false;
+  size_t grec_o_ = 0;
+  uint32_t grec_n_ = 0;
+
   // save the grid chunks of this epoch whose cut happens at or before probe m
   // (chunk k is cut at r_e + (k+2)W - 1); the records are written in place,
   // the common case being every grid chunk of the stream at once
@@ -2242,8 +2372,10 @@ class Resolver {
     const uint32_t kind = indexable_ ? (uint32_t)ZC_CHUNK_NEW : (uint32_t)ZC_BYTES;
     const uint8_t* dead = indexable_ ? dead_.data() + nconf_ : nullptr;
     if (ndead_ == 0 && r_e_ + ks_ * W_ >= s_ && kmax - ks_ >= kParallelRecords) {
-      // every chunk of the run is saved: record o + j is grid chunk ks_ + j
-      fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr);
+      // every chunk of the run is saved: record o + j is grid chunk ks_ + j --
+      // as written ahead, when record o is where chunk ks_ was put
+      if (!(grec_valid_ && o == grec_o_ + ks_ && kmax <= grec_n_))
+        fill_grid_records(rec + o, kmax - ks_, r_e_, ks_, W_, kind, indexable_ ? c_.h_key.p : nullptr);
       gruns_.push_back({o, kmax - ks_, r_e_ + ks_ * W_, kind});
       s_ = r_e_ + kmax * W_;
       ks_ = kmax;
@@ -2533,7 +2665,7 @@ class Resolver {
   const uint8_t* grid_sha() {
     if (!gsha_ready_) {
       sha_launch();  // (if no epoch batch queued it)
-      if (pre_sha_n_) HCK(hipStreamSynchronize(c_.sha_stream));  // the kernel and the copy behind it  // the kernel and the copy behind it
+      if (pre_sha_n_) wait_stream(c_.sha_stream);  // the kernel and the copy behind it  // the kernel and the copy behind it
       gsha_ready_ = true;
     }
     return c_.h_gsha.p;
@@ -3058,6 +3190,7 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_sha, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_grec, hipEventDisableTiming));
     HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
@@ -3085,6 +3218,7 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->ev_sha) (void)hipEventDestroy(c->ev_sha);
+    if (c->ev_grec) (void)hipEventDestroy(c->ev_grec);
     if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -3428,7 +3562,7 @@ int zc_take_records(zc_ctx* c, zc_record* out, size_t cap, size_t* n_out) {
     // between calls every record cut is complete (nrec_done == size): drop
     // the taken prefix once it is most of the vector (amortised O(1) per record)
     if (c->rec_head >= 65536 && 2 * c->rec_head >= c->recs.size() && c->nrec_done == c->recs.size()) {
-      c->recs.erase(c->recs.begin(), c->recs.begin() + c->rec_head);
+      c->recs.erase_front(c->rec_head);
       c->nrec_done -= c->rec_head;
       c->rec_head = 0;
     }

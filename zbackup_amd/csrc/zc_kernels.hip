@@ -970,6 +970,10 @@ struct EpochClear {
   uint32_t* gfilt;  // key filter: zero
   uint32_t gwords;
   unsigned long long* counters;
+  // the scan's two counters (anchors pooled, wave-tiles overflowed): copied to
+  // the host's pinned h_scnt and cleared for the next scan (null: not this batch)
+  unsigned long long* scnt;
+  unsigned long long* h_scnt;
 };
 
 // The first anchor of chunk [c, c + W) at offset >= ZC_ANCHOR_MIN_OFF: its
@@ -1040,6 +1044,10 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
     for (uint64_t j = gt; j < ec.twords; j += gs) ec.tab[j] = ~0ull;
   for (uint64_t j = gt; j < ec.gwords; j += gs) ec.gfilt[j] = 0u;
   if (gt < CNT_LAST) ec.counters[gt] = 0ull;
+  if (ec.scnt && gt < 2) {
+    ec.h_scnt[gt] = ec.scnt[gt];
+    ec.scnt[gt] = 0ull;
+  }
   if (gt >= nchunks) return;
   const uint32_t i = (uint32_t)gt;
   const uint64_t c = r_e + (uint64_t)i * W;
@@ -2969,7 +2977,8 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                               hipStream_t s, hipEvent_t after_meta) {
   const uint32_t nref = nconf + nsref;
   const EpochClear ec{ix.ckeys, nref ? 1u << ix.cbits : 0u, ix.tab,
-                      ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters};
+                      ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters,
+                      ix.scnt, ix.h_scnt};
   // enough threads for the grid chunks, and for the clears at a few words each
   const uint64_t words = (uint64_t)ec.cwords + ec.twords + ec.gwords;
   const uint64_t threads = std::max<uint64_t>({nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
