@@ -9,6 +9,17 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 BIN = os.path.join(HERE, "adapter_main")
 
 
+def build_sidecar_reader(out=os.path.join(HERE, "sidecar_read")):
+    """tests/adapter/sidecar_read.cpp: the adapter's chunk-metadata file reader alone."""
+    cmd = ["g++", "-std=c++11", "-O2", "-Wall", "-Werror",
+           "-I" + os.path.join(HERE, "mock"), "-I" + os.path.join(ROOT, "include"),
+           "-I" + os.path.join(ROOT, "integration"), os.path.join(HERE, "sidecar_read.cpp"),
+           "-o", out, "-L" + os.path.join(ROOT, "zbackup_amd"), "-lzchunk",
+           "-Wl,-rpath," + os.path.join(ROOT, "zbackup_amd"), "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build(out=BIN):
     cmd = ["g++", "-std=c++11", "-O2", "-Wall", "-Werror",
            "-I" + os.path.join(HERE, "mock"), "-I" + os.path.join(ROOT, "include"),

@@ -1055,13 +1055,13 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
   vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
   dead[i] = 0;
   const uint64_t k = pw + rk_acc(data, blk, c, c + W);
+  uint32_t off, gv;
+  uint64_t f;
+  first_anchor(data, av, c, W, off, gv, f);
   key[i] = k;
   // the host's copy (pinned memory, written across PCIe while the kernel
   // runs): no separate copy kernel beside the index build
   if (hkey) hkey[i] = k;
-  uint32_t off, gv;
-  uint64_t f;
-  first_anchor(data, av, c, W, off, gv, f);
   anc_off[i] = off;
   cg[i] = gv;
   cfp[i] = f;
