@@ -15,7 +15,7 @@
 typedef hipError_t (*ScanFn)(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                              uint32_t, unsigned long long*);
 #define DECL(N) extern "C" hipError_t N(const uint8_t*, uint64_t, uint64_t, uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t, unsigned long long*);
-DECL(scan_v_prod) DECL(scan_v_s2) DECL(scan_v_s2_wg1) DECL(scan_v_contig)
+DECL(scan_v_prod) DECL(scan_v_prio1) DECL(scan_v_prio2) DECL(scan_v_prio3)
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 __global__ void fill(uint8_t* d, uint64_t n) {
@@ -38,9 +38,9 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, n);
   struct V { const char* name; ScanFn f; uint64_t* blk; std::vector<float> t; unsigned long long pool; };
   std::vector<V> vs = {{"product (2 x 4 waves, list 144)", scan_v_prod, nullptr, {}, 0},
-                       {"2 x 4 waves, two ring slots", scan_v_s2, nullptr, {}, 0},
-                       {"1 x 4 waves, two ring slots", scan_v_s2_wg1, nullptr, {}, 0},
-                       {"contiguous 8 KiB wave-rounds (probe)", scan_v_contig, nullptr, {}, 0}};
+                       {"hand-off at priority 1", scan_v_prio1, nullptr, {}, 0},
+                       {"hand-off at priority 2", scan_v_prio2, nullptr, {}, 0},
+                       {"hand-off at priority 3", scan_v_prio3, nullptr, {}, 0}};
   uint32_t *dbase, *dcnt, *prel, *pg; unsigned long long* cnt;
   CK(hipMalloc(&dbase, nwt * 4)); CK(hipMalloc(&dcnt, nwt * 4));
   CK(hipMalloc(&prel, nwt * wcap * 4)); CK(hipMalloc(&pg, nwt * wcap * 4)); CK(hipMalloc(&cnt, 64));

@@ -732,6 +732,15 @@ constexpr int kScanWgPerCu = ZC_SCAN_WG_PER_CU_CFG;  // workgroups resident per 
 #define ZC_SCAN_SLOTS_CFG 1
 #endif
 constexpr int kScanSlots = ZC_SCAN_SLOTS_CFG;
+// Wave priority around the hand-off (A/B switch, tools/ubench/scan_geom_ab):
+// a wave waits for its round, reads the slot out and issues the refill at
+// priority kScanPrioHandoff, and hashes at 0, so a wave whose round has landed
+// gets the SIMD's issue slots ahead of the other wave's hashing and the ring
+// is refilled at once (0: no priority changes)
+#ifndef ZC_SCAN_PRIO_CFG
+#define ZC_SCAN_PRIO_CFG 0
+#endif
+constexpr int kScanPrioHandoff = ZC_SCAN_PRIO_CFG;
 static_assert(kScanSlots == 1 || kScanSlots == 2, "one or two ring slots");
 struct ScanLds {
   uint8_t ring[kScanWaves][kScanSlots * 64 * ZC_ROUND];
@@ -803,6 +812,7 @@ __device__ __forceinline__ void scan_body(
   for (uint32_t R = 0; R < nR; ++R) {
     const uint32_t k = R / kRpt;
     const int r = (int)(R - k * kRpt);
+    if constexpr (kScanPrioHandoff > 0) __builtin_amdgcn_s_setprio(kScanPrioHandoff);
     // round R (and, for a half's first round, its warm-up loads) has landed
     // once only what was issued after it is outstanding: the later rounds in
     // flight and the last tile end's stores
@@ -849,6 +859,7 @@ __device__ __forceinline__ void scan_body(
       for (int i = 0; i + 1 < kScanSlots; ++i) after[i] += group(R + kScanSlots);
       issue(R + kScanSlots);
     }
+    if constexpr (kScanPrioHandoff > 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int g = 0; g < kGroups; ++g)
 #pragma unroll
