@@ -1037,13 +1037,17 @@ __device__ __forceinline__ void first_anchor(const uint8_t* __restrict__ data, c
   }
 }
 
-// zc_chunk_meta: thread per grid chunk i of the epoch, start = r_e + i * W:
-// start, visibility time, key, first anchor (offset, gear value, 64-byte
-// fingerprint); the chunk is not yet consumed by a match (dead = 0).  The
-// whole grid also clears the epoch's tables (no separate fills).
+// zc_chunk_meta: per grid chunk i of the epoch, start = r_e + i * W: start,
+// visibility time, key, first anchor (offset, gear value, 8-byte
+// fingerprint); the chunk is not yet consumed by a match (dead = 0).  Two
+// threads per chunk, in different waves: thread i folds the key (W / 1 KiB
+// span digests), thread split + i searches the first anchor (a chain of
+// dependent loads), so the two latency chains overlap instead of adding up
+// (split: a multiple of the block size).  The whole grid also clears the
+// epoch's tables (no separate fills).
 __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
                                      const uint64_t* __restrict__ blk, AnchorView av, uint64_t r_e,
-                                     uint32_t nchunks, uint32_t W, uint64_t pw,
+                                     uint32_t nchunks, uint32_t split, uint32_t W, uint64_t pw,
                                      uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
                                      uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
@@ -1059,43 +1063,50 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
     ec.h_scnt[gt] = ec.scnt[gt];
     ec.scnt[gt] = 0ull;
   }
-  if (gt >= nchunks) return;
-  const uint32_t i = (uint32_t)gt;
-  const uint64_t c = r_e + (uint64_t)i * W;
-  start[i] = c;
-  vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
-  dead[i] = 0;
-  const uint64_t k = pw + rk_acc(data, blk, c, c + W);
-  uint32_t off, gv;
-  uint64_t f;
-  first_anchor(data, av, c, W, off, gv, f);
-  key[i] = k;
-  // the host's copy (pinned memory, written across PCIe while the kernel
-  // runs): no separate copy kernel beside the index build
-  if (hkey) hkey[i] = k;
-  anc_off[i] = off;
-  cg[i] = gv;
-  cfp[i] = f;
+  if (gt < nchunks) {
+    const uint32_t i = (uint32_t)gt;
+    const uint64_t c = r_e + (uint64_t)i * W;
+    start[i] = c;
+    vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
+    dead[i] = 0;
+    const uint64_t k = pw + rk_acc(data, blk, c, c + W);
+    key[i] = k;
+    // the host's copy (pinned memory, written across PCIe while the kernel
+    // runs): no separate copy kernel beside the index build
+    if (hkey) hkey[i] = k;
+  } else if (gt >= split && gt - split < nchunks) {
+    const uint32_t i = (uint32_t)(gt - split);
+    uint32_t off, gv;
+    uint64_t f;
+    first_anchor(data, av, r_e + (uint64_t)i * W, W, off, gv, f);
+    anc_off[i] = off;
+    cg[i] = gv;
+    cfp[i] = f;
+  }
 }
 
-// zc_ref_meta: thread per chunk [start[i], start[i] + W) anywhere in the
-// resident stream: key, first anchor {offset, gear, fingerprint} (the
-// chunks that join the historic index)
+// zc_ref_meta: per chunk [start[i], start[i] + W) anywhere in the resident
+// stream: key, first anchor {offset, gear, fingerprint} (the chunks that
+// join the historic index); the key by thread i, the anchor by thread
+// split + i, as in zc_chunk_meta
 __global__ void zc_ref_meta_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ blk, AnchorView av,
-                                   const uint64_t* __restrict__ starts, uint32_t cnt, uint32_t W, uint64_t pw,
-                                   uint64_t* __restrict__ key, uint32_t* __restrict__ anc_off,
+                                   const uint64_t* __restrict__ starts, uint32_t cnt, uint32_t split, uint32_t W,
+                                   uint64_t pw, uint64_t* __restrict__ key, uint32_t* __restrict__ anc_off,
                                    uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp) {
   ZC_URGENT();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cnt) return;
-  const uint64_t c = starts[i];
-  key[i] = pw + rk_acc(data, blk, c, c + W);
-  uint32_t off, gv;
-  uint64_t f;
-  first_anchor(data, av, c, W, off, gv, f);
-  anc_off[i] = off;
-  cg[i] = gv;
-  cfp[i] = f;
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gt < cnt) {
+    const uint64_t c = starts[gt];
+    key[gt] = pw + rk_acc(data, blk, c, c + W);
+  } else if (gt >= split && gt - split < cnt) {
+    const uint32_t i = (uint32_t)(gt - split);
+    uint32_t off, gv;
+    uint64_t f;
+    first_anchor(data, av, starts[i], W, off, gv, f);
+    anc_off[i] = off;
+    cg[i] = gv;
+    cfp[i] = f;
+  }
 }
 
 // zc_ref_gather: historic entry dst[t] (t < cnt) takes ref src[t] of the
@@ -1144,7 +1155,7 @@ constexpr uint32_t kGFiltWords = 1u << (kGFiltBits - 5);
 
 // ---------------------------------------------------------------------------
 // zc_probe: every anchor of the stream probes the table (key = gear value,
-// confirmed by the 64-byte fingerprint).  A wave takes kProbeWT consecutive
+// confirmed by the 8-byte fingerprint).  A wave takes kProbeWT consecutive
 // wave-tiles and a lane their slots lane, lane + 64, ... (kProbeSlots per
 // wave-tile; slots past that -- dense small-W streams, side-pool wave-tiles --
 // in a second loop; the geometry is chosen at the launch).
@@ -1165,9 +1176,16 @@ struct EpochGrid {
 
 // The probe's candidates are staged per wave in LDS and appended to the
 // global list with one atomic per wave (an incremental backup of unchanged
-// data emits a candidate per 64 KiB: 131,072 same-address atomics made the
-// probe 190 us per 8 GiB); a full stage spills to the global counter.
-constexpr uint32_t kCandStage = 128;
+// data emits a candidate per 64 KiB, 16 per wave: 131,072 same-address
+// atomics made the probe 190 us per 8 GiB); a full stage spills to the
+// global counter.
+constexpr uint32_t kCandStage = 64;
+// The probe's per-wave list of anchors that pass the filters: 128 entries
+// (random data at W = 64 KiB: ~32 per wave).  The probe's LDS is 12 KiB per
+// 4-wave workgroup, so its occupancy is bound by registers, not LDS. With
+// 512 entries it was 41 KiB per workgroup, three workgroups per CU, and the
+// 2048 workgroups of an 8 GiB stream ran in three rounds.
+constexpr uint32_t kPassCap = 128;
 struct CandOut {
   Cand* cand;
   uint64_t cap;
@@ -1257,18 +1275,22 @@ __device__ __forceinline__ void probe_hist(uint64_t pos, uint32_t gk, uint64_t f
 }
 
 template <int kProbeWT, int kProbeSlots>
-__global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
+__global__ void __launch_bounds__(kProbeTPB) __attribute__((amdgpu_waves_per_eu(8))) zc_probe_kernel(
     const uint8_t* __restrict__ data, AnchorView av, uint64_t wt0, uint64_t nwt, const uint64_t* __restrict__ tab,
     uint32_t tbits, const uint32_t* __restrict__ gfilt, const uint32_t* __restrict__ anc_off,
     const uint32_t* __restrict__ cls, const uint64_t* __restrict__ vis, const uint8_t* __restrict__ dead, uint64_t r,
     uint64_t n, uint32_t W, HistTab ht, EpochGrid eg,
     Cand* __restrict__ cand, uint64_t cand_cap, unsigned long long* __restrict__ counters) {
   ZC_URGENT();
-  const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // the wave's index, wave-uniform (its wave-tiles' directory entries and
+  // pointers then live in scalar registers, not in 20-odd VGPRs per lane)
+  const uint64_t gwave = __builtin_amdgcn_readfirstlane(blockIdx.x * (kProbeTPB / 64) + (threadIdx.x >> 6));
   const uint32_t lane = threadIdx.x & 63;
   constexpr int kS = kProbeWT * kProbeSlots;
   __shared__ Cand s_cand[kProbeTPB / 64][kCandStage];
   __shared__ uint32_t s_ncand[kProbeTPB / 64];
+  __shared__ uint2 s_pass[kProbeTPB / 64][kPassCap];
+  __shared__ uint64_t s_fp[kProbeTPB / 64][kPassCap];
   const CandOut co{cand, cand_cap, counters, s_cand[threadIdx.x >> 6], &s_ncand[threadIdx.x >> 6]};
   if (lane == 0) *co.nstage = 0;
   uint64_t wts[kProbeWT];
@@ -1297,54 +1319,61 @@ __global__ void __launch_bounds__(kProbeTPB) zc_probe_kernel(
     f[q] = live[q] && gfilt ? (gfilt[fb >> 5] >> (fb & 31)) & 1u : 0u;
     if (ht.tab) f[q] |= live[q] ? ((ht.filt[fb >> 5] >> (fb & 31)) & 1u) << 1 : 0u;
   }
-  // level 3: the offsets of the anchors that pass; level 4: their
-  // fingerprints (the table slot mixes them in), every lane's in flight at
-  // once; both compacted into the wave's LDS lists {offset in the wave pair |
-  // wave-tile << 24, gear} and {fingerprint}
-  __shared__ uint2 s_pass[kProbeTPB / 64][kS * 64];
-  __shared__ uint64_t s_fp[kProbeTPB / 64][kS * 64];
-  uint2* const lst = s_pass[threadIdx.x >> 6];
-  uint64_t* const lfp = s_fp[threadIdx.x >> 6];
-  uint32_t rel[kS];
+  // the anchors of the wave that pass: at most kPassCap take the compacted
+  // path below; a wave with more (dense or low-entropy content) walks all its
+  // slots in the per-lane loop at the end instead
+  uint32_t npass = 0;
 #pragma unroll
-  for (int q = 0; q < kS; ++q) {
-    const int t = q / kProbeSlots;
-    rel[q] = f[q] ? ta[t].rel[lane + 64u * (q % kProbeSlots)] : 0u;
-  }
-  // (anchors the walks skip -- before r + ZC_ANCHOR_MIN_OFF -- read nothing)
-  uint64_t fpv[kS];
+  for (int q = 0; q < kS; ++q) npass += (uint32_t)__popcll(__ballot(f[q] != 0u));
+  const bool dense = npass > kPassCap;
+  if (!dense) {
+    // level 3: the offsets of the anchors that pass; level 4: their
+    // fingerprints (the table slot mixes them in), every lane's in flight at
+    // once; both compacted into the wave's LDS lists {offset in the wave pair
+    // | wave-tile << 24, gear} and {fingerprint}
+    uint2* const lst = s_pass[threadIdx.x >> 6];
+    uint64_t* const lfp = s_fp[threadIdx.x >> 6];
+    uint32_t rel[kS];
 #pragma unroll
-  for (int q = 0; q < kS; ++q) {
-    const uint64_t pos = (wts[q / kProbeSlots] << ZC_WT_SHIFT) + rel[q];
-    fpv[q] = f[q] && pos >= r + ZC_ANCHOR_MIN_OFF ? anchor_fp(data, pos) : 0ull;
-  }
-  static_assert(ZC_WT_SHIFT < 24 && kProbeWT <= 64, "pass-list packing");
-  uint32_t np = 0;
-#pragma unroll
-  for (int q = 0; q < kS; ++q) {
-    const uint64_t m = __ballot(f[q] != 0u);
-    if (f[q]) {
-      const uint32_t at = np + lane_prefix(m);
-      lst[at] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24 | f[q] << 30, g[q]);
-      lfp[at] = fpv[q];
+    for (int q = 0; q < kS; ++q) {
+      const int t = q / kProbeSlots;
+      rel[q] = f[q] ? ta[t].rel[lane + 64u * (q % kProbeSlots)] : 0u;
     }
-    np += (uint32_t)__popcll(m);
+    // (anchors the walks skip -- before r + ZC_ANCHOR_MIN_OFF -- read nothing)
+    uint64_t fpv[kS];
+#pragma unroll
+    for (int q = 0; q < kS; ++q) {
+      const uint64_t pos = (wts[q / kProbeSlots] << ZC_WT_SHIFT) + rel[q];
+      fpv[q] = f[q] && pos >= r + ZC_ANCHOR_MIN_OFF ? anchor_fp(data, pos) : 0ull;
+    }
+    static_assert(ZC_WT_SHIFT < 24 && kProbeWT <= 64, "pass-list packing");
+    uint32_t np = 0;
+#pragma unroll
+    for (int q = 0; q < kS; ++q) {
+      const uint64_t m = __ballot(f[q] != 0u);
+      if (f[q]) {
+        const uint32_t at = np + lane_prefix(m);
+        lst[at] = make_uint2(rel[q] | (uint32_t)(q / kProbeSlots) << 24 | f[q] << 30, g[q]);
+        lfp[at] = fpv[q];
+      }
+      np += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // level 5: the table walks, one anchor per lane
+    for (uint32_t j = lane; j < np; j += 64) {
+      const uint2 a = lst[j];
+      const uint64_t fp = lfp[j];
+      const uint32_t t = (a.x >> 24) & 63u;
+      const uint64_t pos = ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu);
+      if (a.x & (1u << 30)) probe_anchor(pos, a.y, fp, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, co);
+      if (a.x & (1u << 31)) probe_hist(pos, a.y, fp, ht, r, n, W, co);
+    }
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // level 5: the table walks, one anchor per lane
-  for (uint32_t j = lane; j < np; j += 64) {
-    const uint2 a = lst[j];
-    const uint64_t fp = lfp[j];
-    const uint32_t t = (a.x >> 24) & 63u;
-    const uint64_t pos = ((wt0 + gwave * kProbeWT + t) << ZC_WT_SHIFT) + (a.x & 0xFFFFFFu);
-    if (a.x & (1u << 30)) probe_anchor(pos, a.y, fp, tab, tbits, anc_off, cls, vis, dead, r, n, W, eg, co);
-    if (a.x & (1u << 31)) probe_hist(pos, a.y, fp, ht, r, n, W, co);
-  }
-  // wave-tiles with more anchors than the slots above
+  // wave-tiles with more anchors than the slots above (a dense wave: all)
 #pragma unroll
   for (int t = 0; t < kProbeWT; ++t) {
-    for (uint32_t e = lane + 64u * kProbeSlots; e < ta[t].cnt; e += 64) {
+    for (uint32_t e = lane + (dense ? 0u : 64u * kProbeSlots); e < ta[t].cnt; e += 64) {
       const uint32_t gk = ta[t].g[e];
       const uint32_t fb = gk & ((1u << kGFiltBits) - 1);
       const uint64_t pos = (wts[t] << ZC_WT_SHIFT) + ta[t].rel[e];
@@ -2992,9 +3021,11 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                       ix.scnt, ix.h_scnt};
   // enough threads for the grid chunks, and for the clears at a few words each
   const uint64_t words = (uint64_t)ec.cwords + ec.twords + ec.gwords;
-  const uint64_t threads = std::max<uint64_t>({nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
+  const uint32_t split = (uint32_t)(blocks_for(nsref, 128) * 128);  // the anchor threads' first
+  const uint64_t threads =
+      std::max<uint64_t>({(uint64_t)split + nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
-                     nsref, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
+                     nsref, split, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
                      ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ix.hkey, ec);
   if (after_meta) {
     const hipError_t e = hipEventRecord(after_meta, s);
@@ -3027,8 +3058,9 @@ hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView 
                            uint32_t cnt, uint32_t W, uint64_t pw, uint64_t* key, uint32_t* anc_off, uint32_t* cg,
                            uint64_t* cfp, hipStream_t s) {
   if (!cnt) return hipSuccess;
-  hipLaunchKernelGGL(zc_ref_meta_kernel, dim3(blocks_for(cnt, 128)), dim3(128), 0, s, data, blk, av, starts, cnt, W, pw,
-                     key, anc_off, cg, cfp);
+  const uint32_t split = (uint32_t)(blocks_for(cnt, 128) * 128);
+  hipLaunchKernelGGL(zc_ref_meta_kernel, dim3(blocks_for((uint64_t)split + cnt, 128)), dim3(128), 0, s, data, blk, av,
+                     starts, cnt, split, W, pw, key, anc_off, cg, cfp);
   return hipGetLastError();
 }
 
