@@ -71,6 +71,29 @@ def main():
     for _ in range(k):
         L.zc_chunk_device(ctx, ptr, 0)
     print(f"zc_chunk_device of 0 bytes: {(time.perf_counter() - t0) / k * 1e6:.2f} us per call")
+    ab = os.environ.get("HOST_GAP_AB")  # an engine A/B switch read at zc_create: "NAME" of the env var
+    if ab:
+        os.environ[ab] = "1"
+        bb = BackupCreator(65536, device=0, sha1=False, timing=True)
+        del os.environ[ab]
+        res = {"A": [], "B": []}
+        for _ in range(10):
+            L.zc_chunk_device(bb._ctx, ptr, n)
+        for _ in range(reps):
+            for label, b in (("A", bc), ("B", bb)):
+                t0 = time.perf_counter()
+                assert L.zc_chunk_device(b._ctx, ptr, n) == 0
+                t1 = time.perf_counter()
+                st = b.stats()
+                res[label].append(((t1 - t0) * 1e3, st["scan_ms"], st["meta_ms"]))
+        for label, rs in res.items():
+            rs.sort()
+            m = rs[len(rs) // 2]
+            post = sorted(r[0] - r[1] for r in rs)[len(rs) // 2]
+            meta = sorted(r[2] for r in rs)[len(rs) // 2]
+            print(f"{label} ({ab}={'1' if label == 'B' else 'unset'}): call median {m[0]:.4f} ms, "
+                  f"call - scan median {post * 1e3:.1f} us, meta median {meta * 1e3:.1f} us")
+        bb.close()
     bc.close()
 
 
