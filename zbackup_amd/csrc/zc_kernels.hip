@@ -1520,15 +1520,17 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
       }
     }
   }
-  if (!tab || anc_off[i] == ZC_NO_ANCHOR) return;
+  if (!tab) return;
   // every ref with an anchor enters the anchor table (the probe keeps class
-  // leaders only: classes are not known yet)
-  const uint32_t g = cg[i];
+  // leaders only: classes are not known yet); the ref's three words are read
+  // together (one dependent load level before the inserts, not two)
+  const uint32_t ao = anc_off[i], g = cg[i];
+  const uint64_t fpi = cfp[i];
+  if (ao == ZC_NO_ANCHOR) return;
   const uint32_t fb = g & ((1u << kGFiltBits) - 1);
   atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
   const uint64_t word = ((uint64_t)i << 32) | g;
   const uint32_t mask = (1u << tbits) - 1;
-  const uint64_t fpi = cfp[i];
   for (uint32_t h = table_slot(g, fpi, tbits);; h = (h + 1) & mask) {
     const unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
                                               (unsigned long long)word);
