@@ -272,3 +272,35 @@ def test_utf16_like_content_probe_stays_linear(torch_cuda):
         assert int((kinds == 1).sum()) == half // W, kind
         times[kind] = st["meta_ms"] + st["probe_ms"]
     assert times["utf16"] < 4 * times["random"] + 2.0, times
+
+
+def test_dense_historic_candidates_vs_oracle(torch_cuda):
+    # The device orders historic candidates by position in buckets of about
+    # n / (2 candidates) bytes; a bucket of more than 64 is left unsorted and
+    # the host sorts the whole list (zc_bucket_sort_kernel).  Stream 1 holds
+    # 256 KiB of a 1024-byte period (W = 4096: one chunk, then duplicates of
+    # it).  Stream 2 is 128 MiB of new random bytes around 128 KiB of the same
+    # period at another phase: every historic candidate (one per period) falls
+    # in that 128 KiB, about 128 to a bucket.  The records -- the first
+    # matching window at each point, as BackupCreator finds it -- must equal
+    # the oracle's.
+    from zbackup_amd import BackupCreator
+    W = 4096
+    rng = np.random.default_rng(41)
+    per = np.tile(rng.integers(0, 256, 1024, dtype=np.uint8), 300)
+    s1 = np.concatenate([rng.integers(0, 256, 2 << 20, dtype=np.uint8), per[:256 << 10],
+                         rng.integers(0, 256, 2 << 20, dtype=np.uint8)])
+    s2 = np.concatenate([rng.integers(0, 256, 128 << 20, dtype=np.uint8), per[123:123 + (128 << 10)],
+                         rng.integers(0, 256, 1 << 20, dtype=np.uint8)])
+    t1 = torch_cuda.from_numpy(s1).to("cuda")
+    t2 = torch_cuda.from_numpy(s2).to("cuda")
+    with BackupCreator(W, sha1=True) as bc:
+        bc.chunk_device(t1.data_ptr(), s1.size)
+        r1 = bc.records()
+        bc.chunk_device(t2.data_ptr(), s2.size)
+        got = bc.record_tuples()
+        st = bc.stats()
+    want = oracle.chunk(s2, W, seeds=_seed_tuples(_ids(r1)))
+    assert got == want
+    assert st["candidates"] >= 64
+    assert sum(1 for r in want if r[0] == "D") >= 20  # the period's windows found in the history

@@ -1661,21 +1661,24 @@ __global__ void __launch_bounds__(256) zc_class_verify_kernel(
 // The probe's candidates, checked and ordered on the device (the host walk
 // needs the historic ones key-checked and in position order; checking 131,072
 // of them one by one on the host and radix-sorting them took 2.8 ms of an
-// incremental 8 GiB backup).  Four launches:
+// incremental 8 GiB backup).  Seven launches (launch_cand_order):
 //   zc_cand_split: thread per candidate.  An epoch candidate (pad 0: bytes to
 //     verify against its ref) is appended to out0.  A historic one (pad 1) is
 //     kept iff its window's rolling key equals the entry's -- findChunk's first
 //     test (chunk_index.cc:119-143; the SHA-1 prefix, its second, stays with the
 //     host, which holds the prefixes) -- and takes a rank in its position
 //     bucket p >> bshift (rank ~0: dropped).
-//   zc_bucket_scan: the buckets' exclusive prefix sum (one workgroup).
+//   zc_bucket_sums / zc_bucket_bscan / zc_bucket_offsets: the buckets'
+//     exclusive prefix sum, in three coalesced passes.
 //   zc_cand_scatter: each kept candidate to its bucket's slots, flagged 1 when
 //     its window is a grid chunk whose SHA-1 the side stream computes (joined
 //     by key now, its prefix checked when the digests land), else 2 (the host
 //     hashes the window).
 //   zc_bucket_sort: thread per bucket, its few entries by position; a bucket of
-//     more than kBucketSortMax (pathological: many entries sharing an anchor
-//     and its offset) is left unsorted and flagged, and the host sorts the list.
+//     more than kBucketSortMax (candidates crowded into a small part of the
+//     stream, tests/test_gpu_index_meta.py::test_dense_historic_candidates_vs_oracle)
+//     is left unsorted and flagged, and the host sorts the list.
+//   zc_cand_out: both lists and the counts into the host's pinned buffers.
 constexpr uint32_t kBucketSortMax = 64;
 enum { HC_EPOCH = 0, HC_KEPT = 1, HC_UNSORTED = 2, HC_EPOCH_OUT = 3, HC_LAST = 4 };
 
