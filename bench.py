@@ -619,6 +619,13 @@ def run_rank(args):
     import torch.distributed as dist
 
     world, rank, local = rank_env(args)
+    # one GPU per rank; more ranks than visible GPUs (a rehearsal of the
+    # multi-rank path on a smaller box) share them, and say so
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:
+        print(f"bench.py: rank {rank} shares GPU {local % ndev} ({ndev} visible for {world} ranks)",
+              file=sys.stderr, flush=True)
+        local %= ndev
     torch.cuda.set_device(local)
 
     from zbackup_amd import BackupCreator

@@ -3258,6 +3258,10 @@ int zc_seed_index_meta(zc_ctx* c, const zc_seed* seeds, size_t n, const zc_chunk
   }
   return guarded(c, [&] {
     DeviceGuard g(c->device);
+    // the host arrays hold exactly the entries so far (a call that failed
+    // part-way may have appended some without registering them)
+    c->hkey.resize(c->nhist);
+    c->hsha.resize(16 * (size_t)c->nhist);
     const uint32_t W = c->W, def = anchor_def_of(W);
     // usable metadata by rolling key (then SHA-1 prefix): W-byte chunks of
     // this anchor definition with an anchor where a W-byte chunk can hold one
