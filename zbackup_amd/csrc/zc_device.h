@@ -112,6 +112,19 @@ struct PoolOut {
   uint64_t wt0;
 };
 
+// The first epoch's grid-chunk keys, written by the scan at each wave-tile's
+// end: with W a multiple of the 4 KiB lane span dividing the
+// 256 KiB wave-tile, grid chunk i = [i W, (i + 1) W) is 2^lshift whole lane
+// spans of one wave, and its key 257^W + the Horner fold of its span digests
+// is a reduction over those lanes.  key (device) and hkey (the host's pinned
+// copy) take chunk i at index i; null key: not written.
+struct GridKeysOut {
+  uint64_t* key;
+  uint64_t* hkey;
+  uint64_t pw;      // 257^W
+  uint32_t lshift;  // log2(W / ZC_LSPAN)
+};
+
 // Blocked Bloom filter of the exact screen's large key sets (more than the
 // LDS holds), over the full 64-bit window keys: 2^bits blocks of two 32-bit
 // words (8 bytes, one gather), a key sets three bits in each word
@@ -227,7 +240,15 @@ hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint6
 // the same in pieces: full 2 MiB tiles [tile0, tile0 + ntiles), then the
 // partial last tile (if any); the pieces may run as the stream arrives
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
-                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s);
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s,
+                             GridKeysOut gko = GridKeysOut{nullptr, nullptr, 0, 0});
+// the W for which the scan can write the grid keys (GridKeysOut), else 0
+inline uint32_t scan_key_lshift_or_none(uint32_t W, bool& ok) {
+  ok = W >= (uint32_t)ZC_LSPAN && W % ZC_LSPAN == 0 && ((64u * ZC_LSPAN) % W) == 0;
+  uint32_t l = 0;
+  while (ok && ((uint32_t)ZC_LSPAN << l) < W) ++l;
+  return l;
+}
 hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
                             unsigned long long* counters, hipStream_t s);
 
@@ -279,6 +300,9 @@ struct EpochIndex {
   // the scan's counters (2) to hand to the host (pinned h_scnt) and clear, or null
   unsigned long long* scnt = nullptr;
   unsigned long long* h_scnt = nullptr;
+  // grid chunks [0, key_from) already have key[] and hkey[] (the scan wrote
+  // them: GridKeysOut); the metadata kernel computes the rest
+  uint32_t key_from = 0;
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,

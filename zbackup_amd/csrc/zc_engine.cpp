@@ -554,8 +554,7 @@ struct zc_ctx {
   DevBuf<uint2> cpairs;  // content-class pairs to byte-check
   HostBuf<unsigned long long> h_cnt;
   HostBuf<unsigned long long> h_scnt;  // the scan's counters, read back with the first epoch's batch
-  HostBuf<uint64_t> h_pre;             // digests of the predicted tail pieces
-  DevBuf<uint64_t> d_pre;
+  HostBuf<uint64_t> h_pre;             // digests of the predicted tail pieces (written by the device)
   HostBuf<uint64_t> h_key;  // grid-chunk keys of the current epoch
   HostBuf<uint64_t> h_ra, h_rb, h_rout;  // pinned staging of range-digest batches
 };
@@ -832,6 +831,16 @@ class Resolver {
     spec_hist_.clear();
     acands_.clear();
     hcands_.clear();
+    // the scan writes the first epoch's grid keys (W a multiple of the lane
+    // span dividing the wave-tile; the whole stream resident): their arrays
+    // sized now, before it is queued
+    bool kok = false;
+    key_lshift_ = scan_key_lshift_or_none(W_, kok);
+    scan_keys_ = kok && !windowed_ && indexable_ && n_ >= W_ && n_ / W_ < 0xFFFFFFF0ull;
+    if (scan_keys_) {
+      c_.c_key.ensure(n_ / W_ + 2);
+      c_.h_key.ensure(n_ / W_ + 2);
+    }
     scan_setup();
   }
   // bytes [0, n) of the stream are (being) copied to the device, in order on
@@ -849,8 +858,10 @@ class Resolver {
         scan_open_ = true;
       }
       scnt_pending_ = true;
+      const GridKeysOut gko = scan_keys_ ? GridKeysOut{c_.c_key.p, c_.h_key.p, pow257(W_), key_lshift_}
+                                         : GridKeysOut{nullptr, nullptr, 0, 0};
       HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.scnt.p,
-                            c_.stream));
+                            c_.stream, gko));
       tiles_done_ = t1;
     }
   }
@@ -1159,6 +1170,9 @@ class Resolver {
   std::vector<uint32_t> canc_, cg_;            // cg_: anchor gear value
   std::vector<uint8_t> dead_;
   uint64_t ndead_ = 0;  // refs of this epoch consumed by same-grid matches
+  bool scan_keys_ = false;    // the scan writes the first epoch's grid keys (begin)
+  hipEvent_t grec_ev_ = nullptr;  // the grid records' keys are in once this event is
+  uint32_t key_lshift_ = 0;   // log2 of the lane spans per grid chunk
   static constexpr uint64_t kParallelRecords = 32768;
   uint32_t nconf_ = 0, nspec_ = 0, nref_ = 0;
   uint64_t ks_ = 0;  // next grid chunk of this epoch to save
@@ -1286,6 +1300,7 @@ class Resolver {
     if (scan_open_) {
       if (!(c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_idx, c_.stream));
       side_wait_ = (c_.flags & ZC_FLAG_TIMING) ? c_.ev1 : c_.ev_idx;
+      scan_end_ev_ = side_wait_;
     }
     scan_checked_ = false;
   }
@@ -1361,6 +1376,7 @@ class Resolver {
   bool scnt_pending_ = false;  // scans queued whose counters are still on the device
   bool meta_from_scan_ = false;  // ev1 marks the end of scan launches queued for this batch
   hipEvent_t side_wait_ = nullptr;  // the copy stream's next work waits for this scan end
+  hipEvent_t scan_end_ev_ = nullptr;  // recorded at the last scan's end (scan_finish)
 
   // ---------------------------------------------------------------- epoch
   // One epoch = one grid origin r_e.  Device work is queued back to back
@@ -1418,6 +1434,12 @@ class Resolver {
         }
       }
       c_.h_cnt.ensure(CNT_LAST);
+      // the first epoch's grid chunks inside the scanned full tiles have their
+      // keys from the scan (begin: scan_keys_), if the arrays still hold them
+      const uint32_t key_from =
+          scan_keys_ && r_e_ == 0 && nconf_ == 0 && c_.c_key.cap >= nref_ && c_.h_key.cap >= nsref
+              ? (uint32_t)std::min<uint64_t>(nsref, tiles_done_ * ZC_STILE / W_)
+              : 0u;
       if (nref_) {
         c_.c_start.ensure(nref_);
         c_.c_key.ensure(nref_);
@@ -1446,6 +1468,7 @@ class Resolver {
                         c_.ckeys.p,   tbits,      anchors ? c_.tab.p : nullptr, tbits,
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
                         pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_, nsref ? c_.h_key.p : nullptr};
+        ix.key_from = key_from;
         if (scnt_pending_) {  // the chunk-metadata kernel hands the scan's counters over
           ix.scnt = c_.scnt.p;
           ix.h_scnt = c_.h_scnt.p;
@@ -1453,8 +1476,11 @@ class Resolver {
         }
         grec_valid_ = false;
         grec_ = !windowed_ && indexable_ && nsref >= kGridRecordsMin;
+        // every grid key from the scan: the records can be written once the
+        // scan is in (no marker inside the batch: one costs it ~6 us)
+        grec_ev_ = key_from == nsref && scan_end_ev_ ? scan_end_ev_ : c_.ev_grec;
         HCK(launch_epoch_index(d_, n_, blk_v(), av(), r_e_, nconf_, nsref, W_, pow257(W_), ix, c_.stream,
-                               grec_ ? c_.ev_grec : nullptr));
+                               grec_ && grec_ev_ == c_.ev_grec ? c_.ev_grec : nullptr));
         dev_r_e_ = r_e_;
         dev_nconf_ = nconf_;
         dev_nspec_ = nsref;
@@ -1499,7 +1525,7 @@ class Resolver {
       if (grec_) {
         const size_t o_e = c_.recs.size();
         c_.recs.reserve(o_e + nsref + 64);
-        wait_event(c_.ev_grec);
+        wait_event(grec_ev_);
         fill_grid_records(c_.recs.data() + o_e, nsref, r_e_, 0, W_, ZC_CHUNK_NEW, c_.h_key.p);
         grec_valid_ = true;
         grec_o_ = o_e;
@@ -1625,10 +1651,10 @@ class Resolver {
     }
     if (pre_a_.empty()) return;
     const uint32_t nr = (uint32_t)pre_a_.size();
-    c_.d_pre.ensure(nr);
+    // the digests go straight into pinned host memory: a copy behind the
+    // kernel ran beside the batch's index insert and slowed it (18-26 us)
     c_.h_pre.ensure(nr);
-    HCK(launch_range_digest_small(d_, n_, blk_v(), pre_a_.data(), pre_b_.data(), nr, c_.d_pre.p, c_.copy_stream));
-    HCK(hipMemcpyAsync(c_.h_pre.p, c_.d_pre.p, nr * sizeof(uint64_t), hipMemcpyDeviceToHost, c_.copy_stream));
+    HCK(launch_range_digest_small(d_, n_, blk_v(), pre_a_.data(), pre_b_.data(), nr, c_.h_pre.p, c_.copy_stream));
     pre_ready_ = true;  // read after the epoch's copy-stream synchronisation
   }
 
@@ -3152,8 +3178,7 @@ size_t ctx_hbm_bytes(const zc_ctx& c) {
              c.c_vis.bytes() + c.c_anc.bytes() + c.c_g.bytes() + c.c_dead.bytes() + c.ckeys.bytes() +
              c.c_cls.bytes() + c.tab.bytes() + c.gfilt.bytes() + c.cand.bytes() + c.va.bytes() + c.vb.bytes() +
              c.dout.bytes() + c.vlen.bytes() + c.vok.bytes() + c.sha_out.bytes() + c.f32.bytes() + c.fbits.bytes() +
-             c.fbits17.bytes() + c.fwt_off.bytes() + c.fwt_cnt.bytes() + c.runs.bytes() + c.ancless.bytes() +
-             c.d_pre.bytes();
+             c.fbits17.bytes() + c.fwt_off.bytes() + c.fwt_cnt.bytes() + c.runs.bytes() + c.ancless.bytes();
   return b;
 }
 

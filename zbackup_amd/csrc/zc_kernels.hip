@@ -608,15 +608,35 @@ __device__ __forceinline__ PieceHits piece_hits(const WaveList& wl, uint32_t i, 
 // the next round's wait can leave them be.  A wave-tile whose list or pool
 // share overflowed is marked for the exact rescan (zc_anchor_rescan) and
 // stores no anchors.
+// (gko.key: also the grid-chunk keys of the wave-tile: each lane folds its
+// span digests, weights them by 257^(4 KiB x the lanes after it in its chunk)
+// -- lane_w -- and the chunk's lanes add up; the chunk's first lane stores the
+// key, always lane 0 among them, so both store instructions always issue and
+// are counted)
 __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane, int32_t lo_thr,
                                                   const uint64_t (&bk)[kDigests], const WaveList& wl,
                                                   uint32_t last, uint64_t* __restrict__ blk, PoolOut po,
-                                                  uint32_t& acc_pool, uint32_t& acc_over) {
+                                                  uint32_t& acc_pool, uint32_t& acc_over, const GridKeysOut& gko,
+                                                  uint64_t span_m, uint64_t lane_w) {
   uint4* bo = (uint4*)(blk + span0 / ZC_SPAN);
 #pragma unroll
   for (int t = 0; t < kDigests / 2; ++t)
     bo[t] = make_uint4((uint32_t)bk[2 * t], (uint32_t)(bk[2 * t] >> 32), (uint32_t)bk[2 * t + 1],
                        (uint32_t)(bk[2 * t + 1] >> 32));
+  uint32_t nkey = 0;
+  if (gko.key) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int t = 0; t < kDigests; ++t) acc = acc * span_m + bk[t];
+    acc *= lane_w;
+    for (uint32_t d = 1; d < (1u << gko.lshift); d <<= 1) acc += __shfl_xor(acc, (int)d, 64);
+    if ((lane & ((1u << gko.lshift) - 1)) == 0) {
+      const uint64_t i = (span0 / ZC_LSPAN) >> gko.lshift;  // grid chunk i (the first epoch: r_e = 0)
+      gko.key[i] = gko.pw + acc;
+      gko.hkey[i] = gko.pw + acc;
+    }
+    nkey = 2;
+  }
   const uint64_t wt = span0 >> ZC_WT_SHIFT;
   const uint32_t base = (uint32_t)(wt - po.wt0) * po.wcap;
   uint32_t tot = 0, excl = 0, nst = 0;
@@ -705,7 +725,7 @@ __device__ __forceinline__ uint32_t scan_tile_end(uint64_t span0, uint32_t lane,
   // (one same-address atomic per wave-tile serialised in L2: 1.5 % of the scan)
   acc_pool += over ? 0u : tot;
   acc_over += over ? 1u : 0u;
-  return kDigests / 2 + __builtin_amdgcn_readfirstlane(nst) + 2;
+  return kDigests / 2 + __builtin_amdgcn_readfirstlane(nst) + 2 + nkey;
 }
 
 // Every wave walks whole wave-tiles (256 KiB, 64 lane spans) on its own:
@@ -750,7 +770,8 @@ struct ScanLds {
 static_assert(kScanWgPerCu * sizeof(ScanLds) <= 160 * 1024, "the scan workgroups of a CU fit its LDS");
 __device__ __forceinline__ void scan_body(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t wt0, uint64_t nwt, int32_t lo_thr,
-    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L) {
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, ScanLds& L,
+    GridKeysOut gko = GridKeysOut{nullptr, nullptr, 0, 0}) {
   constexpr uint32_t kRpt = kRounds;  // rounds per wave-tile
   constexpr uint32_t kWpt = ZC_SCAN_TPB / 64;  // wave-tiles per 2 MiB tile
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -807,6 +828,10 @@ __device__ __forceinline__ void scan_body(
   uint64_t span0 = 0;
   uint32_t last = kNoEntry;  // this lane's newest entry in the wave's list
   uint32_t acc_pool = 0, acc_over = 0;  // wave-uniform: anchors stored, wave-tiles overflowed
+  // the grid keys' multipliers: 257^1 KiB, and this lane's weight in its chunk
+  const uint64_t span_m = span_mul();
+  const uint64_t lane_w =
+      gko.key ? pow257_dev((uint64_t)ZC_LSPAN * (((1u << gko.lshift) - 1) - (lane & ((1u << gko.lshift) - 1)))) : 0;
 
 #pragma unroll 1
   for (uint32_t R = 0; R < nR; ++R) {
@@ -873,7 +898,8 @@ __device__ __forceinline__ void scan_body(
       s.hlo = s.hhi = 0;
     }
     if (r == kRounds - 1) {
-      const uint32_t ns = scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over);
+      const uint32_t ns =
+          scan_tile_end(span0, lane, lo_thr, bk, wl, last, blk, po, acc_pool, acc_over, gko, span_m, lane_w);
 #pragma unroll
       for (int i = 0; i < kScanSlots; ++i) after[i] += ns;
     }
@@ -887,9 +913,9 @@ __device__ __forceinline__ void scan_body(
 // (__launch_bounds__' second argument: at least kScanWgPerCu waves per SIMD)
 __global__ void __launch_bounds__(64 * kScanWaves, kScanWgPerCu) zc_scan_kernel(
     const uint8_t* __restrict__ data, uint64_t n, uint64_t wt0, uint64_t nwt, int32_t lo_thr,
-    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters) {
+    uint64_t* __restrict__ blk, PoolOut po, unsigned long long* __restrict__ counters, GridKeysOut gko) {
   __shared__ ScanLds lds;
-  scan_body(data, n, wt0, nwt, lo_thr, blk, po, counters, lds);
+  scan_body(data, n, wt0, nwt, lo_thr, blk, po, counters, lds, gko);
 }
 // the stream's last, partial tile: one 256-thread block per wave-tile, a
 // 1 KiB sub-span per thread (block digests and anchors)
@@ -1051,7 +1077,8 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
                                      uint64_t* __restrict__ start, uint64_t* __restrict__ vis,
                                      uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
-                                     uint32_t* __restrict__ anc_off, uint64_t* __restrict__ hkey, EpochClear ec) {
+                                     uint32_t* __restrict__ anc_off, uint64_t* __restrict__ hkey, uint32_t key_from,
+                                     EpochClear ec) {
   ZC_URGENT();
   const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
@@ -1069,11 +1096,13 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
     start[i] = c;
     vis[i] = c + 2ull * W - 1;  // cut in the iteration whose probe is at c + 2W - 1
     dead[i] = 0;
-    const uint64_t k = pw + rk_acc(data, blk, c, c + W);
-    key[i] = k;
-    // the host's copy (pinned memory, written across PCIe while the kernel
-    // runs): no separate copy kernel beside the index build
-    if (hkey) hkey[i] = k;
+    if (i >= key_from) {  // (below: the scan wrote the key and the host's copy)
+      const uint64_t k = pw + rk_acc(data, blk, c, c + W);
+      key[i] = k;
+      // the host's copy (pinned memory, written across PCIe while the kernel
+      // runs): no separate copy kernel beside the index build
+      if (hkey) hkey[i] = k;
+    }
   } else if (gt >= split && gt - split < nchunks) {
     const uint32_t i = (uint32_t)(gt - split);
     uint32_t off, gv;
@@ -2978,14 +3007,16 @@ static int cu_count() {
 }
 
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
-                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s) {
+                             uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s,
+                             GridKeysOut gko) {
   if (!ntiles) return hipSuccess;
+  if (gko.key && (!gko.hkey || ((uint64_t)ZC_LSPAN << gko.lshift) > (1ull << ZC_WT_SHIFT))) return hipErrorInvalidValue;
   // the tiles' wave-tiles, a wave each at a time, kScanWgPerCu workgroups per CU
   const uint64_t wt0 = tile0 * (ZC_SCAN_TPB / 64), nwt = ntiles * (ZC_SCAN_TPB / 64);
   const unsigned grid = (unsigned)std::min<uint64_t>((nwt + kScanWaves - 1) / kScanWaves,
                                                      (uint64_t)cu_count() * kScanWgPerCu);
   hipLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(64 * kScanWaves), 0, s, data, n, wt0, nwt, anchor_lo, blk,
-                     po, counters);
+                     po, counters, gko);
   return hipGetLastError();
 }
 
@@ -3031,7 +3062,7 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
       std::max<uint64_t>({(uint64_t)split + nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
                      nsref, split, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
-                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ix.hkey, ec);
+                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ix.hkey, ix.key_from, ec);
   if (after_meta) {
     const hipError_t e = hipEventRecord(after_meta, s);
     if (e != hipSuccess) return e;
