@@ -241,7 +241,8 @@ hipError_t launch_scan(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint6
 // partial last tile (if any); the pieces may run as the stream arrives
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
                              uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s,
-                             GridKeysOut gko = GridKeysOut{nullptr, nullptr, 0, 0});
+                             GridKeysOut gko = GridKeysOut{nullptr, nullptr, 0, 0}, hipEvent_t start = nullptr,
+                             hipEvent_t stop = nullptr);
 // the W for which the scan can write the grid keys (GridKeysOut), else 0
 inline uint32_t scan_key_lshift_or_none(uint32_t W, bool& ok) {
   ok = W >= (uint32_t)ZC_LSPAN && W % ZC_LSPAN == 0 && ((64u * ZC_LSPAN) % W) == 0;
@@ -249,8 +250,12 @@ inline uint32_t scan_key_lshift_or_none(uint32_t W, bool& ok) {
   while (ok && ((uint32_t)ZC_LSPAN << l) < W) ++l;
   return l;
 }
+// (start / stop: events the launch itself records at the kernel's start and
+// end -- hipExtLaunchKernel -- in place of markers around it: a marker between
+// the scan and the next kernel cost ~7 us.  The tail returns whether it launched.)
 hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
-                            unsigned long long* counters, hipStream_t s);
+                            unsigned long long* counters, hipStream_t s, hipEvent_t start = nullptr,
+                            hipEvent_t stop = nullptr);
 
 // exact rescan of the wave-tiles the scan marked overflowed (directory count
 // 0xFFFFFFFF): pass 0 sets cnt[tiles[i]] to the exact count; pass 1 writes the
@@ -322,6 +327,9 @@ hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView 
                            uint64_t* cfp, hipStream_t s);
 // key, first anchor, gear and fingerprint of entry dst[t] = those of ref src[t]
 // (t < cnt): chunks joining the historic index whose metadata an epoch computed
+// the batch's counters into the host's pinned copy, by a kernel queued behind
+// the batch (a runtime copy there started ~6 us after the last kernel ended)
+hipError_t launch_counters_out(const unsigned long long* counters, unsigned long long* h_cnt, hipStream_t s);
 hipError_t launch_ref_gather(const uint32_t* src, const uint32_t* dst, uint32_t cnt, const uint64_t* ckey,
                              const uint32_t* canc, const uint32_t* cg, const uint64_t* cfp, uint64_t* key,
                              uint32_t* anc, uint32_t* g, uint64_t* fp, hipStream_t s);

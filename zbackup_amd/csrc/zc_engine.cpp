@@ -849,19 +849,25 @@ class Resolver {
     n_ = n;
     c_.stats.bytes = n;
   }
-  // launch the scan of the full 2 MiB tiles below m
-  void scan_upto(uint64_t m) {
+  // the event that marks the end of the stream's scan (scan_finish)
+  hipEvent_t scan_end_event() const { return (c_.flags & ZC_FLAG_TIMING) ? c_.ev1 : c_.ev_idx; }
+  // launch the scan of the full 2 MiB tiles below m; `last`: no scan kernel
+  // follows this one, so it records the scan-end event itself
+  void scan_upto(uint64_t m, bool last = false) {
     const uint64_t t1 = std::min(m, n_) / ZC_STILE;
     if (t1 > tiles_done_) {
+      hipEvent_t start = nullptr;
       if (!scan_open_) {
-        if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
+        if (c_.flags & ZC_FLAG_TIMING) start = c_.ev0;
         scan_open_ = true;
       }
       scnt_pending_ = true;
       const GridKeysOut gko = scan_keys_ ? GridKeysOut{c_.c_key.p, c_.h_key.p, pow257(W_), key_lshift_}
                                          : GridKeysOut{nullptr, nullptr, 0, 0};
+      hipEvent_t stop = last ? scan_end_event() : nullptr;
       HCK(launch_scan_tiles(d_, n_, tiles_done_, t1 - tiles_done_, anchor_lo_, blk_v(), pool_out(), c_.scnt.p,
-                            c_.stream, gko));
+                            c_.stream, gko, start, stop));
+      scan_end_recorded_ = stop != nullptr;
       tiles_done_ = t1;
     }
   }
@@ -895,13 +901,18 @@ class Resolver {
   void run_final() {
     const auto t0 = Clock::now();
     if (n_ > 0) {
-      scan_upto(n_);
-      if (n_ % ZC_STILE && !scan_open_) {
-        if (c_.flags & ZC_FLAG_TIMING) HCK(hipEventRecord(c_.ev0, c_.stream));
-        scan_open_ = true;
+      const bool tail = n_ % ZC_STILE != 0;
+      scan_upto(n_, !tail);
+      if (tail) {
+        hipEvent_t start = nullptr;
+        if (!scan_open_) {
+          if (c_.flags & ZC_FLAG_TIMING) start = c_.ev0;
+          scan_open_ = true;
+        }
+        scnt_pending_ = true;
+        HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.scnt.p, c_.stream, start, scan_end_event()));
+        scan_end_recorded_ = true;
       }
-      scnt_pending_ = true;
-      HCK(launch_scan_tail(d_, n_, anchor_lo_, blk_v(), pool_out(), c_.scnt.p, c_.stream));
       if (!windowed_) pre_sha();
       scan_finish();
       lim_ = n_;
@@ -1134,6 +1145,7 @@ class Resolver {
   Clock::time_point t_begin_;
   uint64_t tiles_done_ = 0;  // full scan tiles launched
   bool scan_open_ = false;   // scan launches queued since the last scan_finish
+  bool scan_end_recorded_ = false;  // the last scan launch records the scan-end event itself
   uint64_t chk_wt_ = 0;      // wave-tiles below are checked for overflow
   uint64_t side_used_ = 0;   // entries of the side pool in use
   uint32_t hist0_ = 0;       // historic entries when the stream began
@@ -1293,15 +1305,16 @@ class Resolver {
   // one did (scan_check).  Overflowed wave-tiles read as empty until then.
   void scan_finish() {
     meta_from_scan_ = scan_open_;
-    if ((c_.flags & ZC_FLAG_TIMING) && scan_open_) HCK(hipEventRecord(c_.ev1, c_.stream));
     // the side stream's work of the next epoch (tail digests) needs the scan's
-    // span digests only: it waits for this marker, not for one inside the
-    // epoch's batch (a marker between two kernels costs the batch ~7 us)
+    // span digests only: it waits for the scan-end event, not for one inside
+    // the epoch's batch.  The last scan launch records it itself when it is
+    // known to be the last (scan_upto / run_final); else it is a marker here.
     if (scan_open_) {
-      if (!(c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_idx, c_.stream));
-      side_wait_ = (c_.flags & ZC_FLAG_TIMING) ? c_.ev1 : c_.ev_idx;
+      if (!scan_end_recorded_) HCK(hipEventRecord(scan_end_event(), c_.stream));
+      side_wait_ = scan_end_event();
       scan_end_ev_ = side_wait_;
     }
+    scan_end_recorded_ = false;
     scan_checked_ = false;
   }
   // the scan's counters to h_scnt (and cleared) unless the next batch's
@@ -1510,8 +1523,9 @@ class Resolver {
       // spinning by the time the batch is in
       if (nsref >= kParallelRecordsMin) SpinTeam::get().arm();
       const bool first = !scan_checked_ && meta_from_scan_;  // this batch also waits for the scan
+      HCK(launch_counters_out(c_.counters.p, c_.h_cnt.p, c_.stream));
+      // (after the read-back kernel: a marker between two kernels costs ~6 us)
       if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
-      d2h(c_, c_.h_cnt.p, c_.counters.p, CNT_LAST);
       // the grid SHA-1 behind the batch's read-back too: that copy runs alone
       // (beside the SHA-1 it took 14 us instead of 6), the SHA-1 a few us later
       sha_launch();

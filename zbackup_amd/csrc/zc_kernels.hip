@@ -24,6 +24,7 @@
 //   zc_sha1        SHA-1 of byte ranges (chunk ids, backup_creator.cc:130-131).
 //
 // No MFMA: this is integer/byte work bound by HBM reads.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -3008,23 +3009,32 @@ static int cu_count() {
 
 hipError_t launch_scan_tiles(const uint8_t* data, uint64_t n, uint64_t tile0, uint64_t ntiles, int32_t anchor_lo,
                              uint64_t* blk, PoolOut po, unsigned long long* counters, hipStream_t s,
-                             GridKeysOut gko) {
+                             GridKeysOut gko, hipEvent_t start, hipEvent_t stop) {
   if (!ntiles) return hipSuccess;
   if (gko.key && (!gko.hkey || ((uint64_t)ZC_LSPAN << gko.lshift) > (1ull << ZC_WT_SHIFT))) return hipErrorInvalidValue;
   // the tiles' wave-tiles, a wave each at a time, kScanWgPerCu workgroups per CU
   const uint64_t wt0 = tile0 * (ZC_SCAN_TPB / 64), nwt = ntiles * (ZC_SCAN_TPB / 64);
   const unsigned grid = (unsigned)std::min<uint64_t>((nwt + kScanWaves - 1) / kScanWaves,
                                                      (uint64_t)cu_count() * kScanWgPerCu);
-  hipLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(64 * kScanWaves), 0, s, data, n, wt0, nwt, anchor_lo, blk,
-                     po, counters, gko);
+  if (start || stop)
+    hipExtLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(64 * kScanWaves), 0, s, start, stop, 0, data, n, wt0, nwt,
+                          anchor_lo, blk, po, counters, gko);
+  else
+    hipLaunchKernelGGL(zc_scan_kernel, dim3(grid), dim3(64 * kScanWaves), 0, s, data, n, wt0, nwt, anchor_lo, blk,
+                       po, counters, gko);
   return hipGetLastError();
 }
 
 hipError_t launch_scan_tail(const uint8_t* data, uint64_t n, int32_t anchor_lo, uint64_t* blk, PoolOut po,
-                            unsigned long long* counters, hipStream_t s) {
-  if (n % ZC_STILE)
-    hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(ZC_SCAN_TPB / 64), dim3(ZC_WT_BLOCK), 0, s, data, n, n / ZC_STILE,
-                       anchor_lo, blk, po, counters);
+                            unsigned long long* counters, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+  if (n % ZC_STILE) {
+    if (start || stop)
+      hipExtLaunchKernelGGL(zc_scan_tail_kernel, dim3(ZC_SCAN_TPB / 64), dim3(ZC_WT_BLOCK), 0, s, start, stop, 0, data,
+                            n, (uint64_t)(n / ZC_STILE), anchor_lo, blk, po, counters);
+    else
+      hipLaunchKernelGGL(zc_scan_tail_kernel, dim3(ZC_SCAN_TPB / 64), dim3(ZC_WT_BLOCK), 0, s, data, n, n / ZC_STILE,
+                         anchor_lo, blk, po, counters);
+  }
   return hipGetLastError();
 }
 
@@ -3097,6 +3107,18 @@ hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView 
   const uint32_t split = (uint32_t)(blocks_for(cnt, 128) * 128);
   hipLaunchKernelGGL(zc_ref_meta_kernel, dim3(blocks_for((uint64_t)split + cnt, 128)), dim3(128), 0, s, data, blk, av,
                      starts, cnt, split, W, pw, key, anc_off, cg, cfp);
+  return hipGetLastError();
+}
+
+__global__ void zc_counters_out_kernel(const unsigned long long* __restrict__ counters,
+                                       unsigned long long* __restrict__ h_cnt) {
+  ZC_URGENT();
+  if (threadIdx.x < CNT_LAST) h_cnt[threadIdx.x] = counters[threadIdx.x];
+}
+
+hipError_t launch_counters_out(const unsigned long long* counters, unsigned long long* h_cnt, hipStream_t s) {
+  static_assert(CNT_LAST <= 64, "one wave");
+  hipLaunchKernelGGL(zc_counters_out_kernel, dim3(1), dim3(64), 0, s, counters, h_cnt);
   return hipGetLastError();
 }
 
