@@ -308,6 +308,10 @@ struct EpochIndex {
   // grid chunks [0, key_from) already have key[] and hkey[] (the scan wrote
   // them: GridKeysOut); the metadata kernel computes the rest
   uint32_t key_from = 0;
+  // the class table, anchor table and filter are empty already (cleared at
+  // the end of the last stream): with every key in, the metadata kernel also
+  // does the index inserts (no separate clear, no zc_index_insert launch)
+  bool tables_clean = false;
 };
 hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* blk, AnchorView av, uint64_t r_e,
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
@@ -320,6 +324,10 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
 hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, uint32_t W, const EpochIndex& ix,
                             uint32_t nref, hipStream_t s);
 uint32_t probe_filter_words();
+// the epoch tables emptied (class table and anchor table to all ones, filter
+// to zero), at the end of a stream, while the host finishes it
+hipError_t launch_tables_clear(uint64_t* ckeys, uint64_t cwords, uint64_t* tab, uint64_t twords, uint32_t* gfilt,
+                               uint64_t gwords, hipStream_t s);
 
 // key and first anchor of chunks [starts[i], starts[i] + W) (resident)
 hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView av, const uint64_t* starts,

@@ -418,6 +418,8 @@ struct zc_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_meta = nullptr, ev_in = nullptr, ev_idx = nullptr;
   hipEvent_t ev_sha = nullptr;  // the grid chunks' SHA-1 (sha_stream) are complete
   hipEvent_t ev_grec = nullptr;  // an epoch's chunk metadata is in: its grid records can be written
+  hipEvent_t ev_copy = nullptr;  // the copy stream's work queued with an epoch's batch is done
+  hipEvent_t ev_batch = nullptr;  // an epoch's batch is done (untimed)
   std::string err;
 
   // host feed
@@ -502,6 +504,9 @@ struct zc_ctx {
   DevBuf<uint32_t> co_bcnt, co_boff, co_bsum, co_rank;
   DevBuf<Cand> co_out0, co_out;
   DevBuf<unsigned long long> co_hc;
+  // the epoch tables (ckeys, tab, gfilt) are empty: cleared at the end of the
+  // last stream; the next first epoch inserts without clearing (fused)
+  bool tables_clean = false;
   HostBuf<unsigned long long> h_co_hc;
   HostBuf<Cand> h_hist_cand;  // the historic candidates, key-checked and in position order
   HostBuf<uint32_t> h_cls;  // the epoch's content classes (likewise)
@@ -849,6 +854,14 @@ class Resolver {
     n_ = n;
     c_.stats.bytes = n;
   }
+  // the epoch tables emptied on the context's stream (whole capacities)
+  void clear_tables() {
+    if (c_.tables_clean || (!c_.ckeys.p && !c_.tab.p)) return;
+    if (c_.ckeys.cap % 2 || c_.tab.cap % 2 || c_.gfilt.cap % 4) return;  // (not whole 16-byte units: left dirty)
+    HCK(launch_tables_clear(c_.ckeys.p, c_.ckeys.p ? c_.ckeys.cap : 0, c_.tab.p, c_.tab.p ? c_.tab.cap : 0,
+                            c_.gfilt.p, c_.gfilt.p ? c_.gfilt.cap : 0, c_.stream));
+    c_.tables_clean = true;
+  }
   // the event that marks the end of the stream's scan (scan_finish)
   hipEvent_t scan_end_event() const { return (c_.flags & ZC_FLAG_TIMING) ? c_.ev1 : c_.ev_idx; }
   // launch the scan of the full 2 MiB tiles below m; `last`: no scan kernel
@@ -925,6 +938,7 @@ class Resolver {
       }
     }
     finalize_records(true);
+    clear_tables();  // (normally done after the last epoch's probe already)
     const double ms = ms_since(t0);
     c_.stats.total_ms += ms;
     // the resolver's work overlaps the scan's tail (nothing waits for the scan
@@ -1439,6 +1453,7 @@ class Resolver {
       // probe 69 -> 59 us; an eighth saves no more than its larger clear costs)
       uint32_t tbits = 10;
       while ((1u << tbits) < 4u * nref_) ++tbits;
+      const void* const tabs0[3] = {c_.tab.p, c_.gfilt.p, c_.ckeys.p};
       if (anchors) {
         c_.cand.ensure(std::max<uint64_t>(1u << 16, nref_));
         if (nref_) {
@@ -1474,6 +1489,7 @@ class Resolver {
         }
         // content classes: identical refs share one leader in the table
         c_.ckeys.ensure(1u << tbits);
+        if (c_.tab.p != tabs0[0] || c_.gfilt.p != tabs0[1] || c_.ckeys.p != tabs0[2]) c_.tables_clean = false;
         c_.c_cls.ensure(nref_);
         c_.cpairs.ensure(nref_);
         ix = EpochIndex{c_.c_start.p, c_.c_vis.p, c_.c_dead.p, c_.c_key.p,
@@ -1482,6 +1498,8 @@ class Resolver {
                         c_.gfilt.p,   c_.ancless.p, c_.counters.p, c_.cpairs.p,
                         pre_sha_n_ ? c_.h_gsha.p : nullptr, pre_sha_n_, nsref ? c_.h_key.p : nullptr};
         ix.key_from = key_from;
+        ix.tables_clean = c_.tables_clean;
+        c_.tables_clean = false;  // this epoch fills them
         if (scnt_pending_) {  // the chunk-metadata kernel hands the scan's counters over
           ix.scnt = c_.scnt.p;
           ix.h_scnt = c_.h_scnt.p;
@@ -1519,13 +1537,20 @@ class Resolver {
         side_wait_ = nullptr;
       }
       predict_tail();
+      // what the copy stream holds now (the tail digests): waited for by this
+      // event, not by querying the stream, which reported it busy ~17 us
+      // after its last kernel had ended
+      HCK(hipEventRecord(c_.ev_copy, c_.copy_stream));
       // the walk writes this many grid records at once: have the record team
       // spinning by the time the batch is in
       if (nsref >= kParallelRecordsMin) SpinTeam::get().arm();
       const bool first = !scan_checked_ && meta_from_scan_;  // this batch also waits for the scan
       HCK(launch_counters_out(c_.counters.p, c_.h_cnt.p, c_.stream));
-      // (after the read-back kernel: a marker between two kernels costs ~6 us)
-      if (first && (c_.flags & ZC_FLAG_TIMING)) HCK(hipEventRecord(c_.ev_meta, c_.stream));
+      // the batch's end, waited for by this event (after the read-back kernel:
+      // a marker between two kernels costs ~6 us); with timing it is ev_meta
+      hipEvent_t batch_ev = c_.ev_batch;
+      if (first && (c_.flags & ZC_FLAG_TIMING)) batch_ev = c_.ev_meta;
+      HCK(hipEventRecord(batch_ev, c_.stream));
       // the grid SHA-1 behind the batch's read-back too: that copy runs alone
       // (beside the SHA-1 it took 14 us instead of 6), the SHA-1 a few us later
       sha_launch();
@@ -1545,8 +1570,8 @@ class Resolver {
         grec_o_ = o_e;
         grec_n_ = nsref;
       }
-      sync(c_);
-      wait_stream(c_.copy_stream);
+      wait_event(batch_ev);
+      wait_event(c_.ev_copy);
       if (scan_check()) {  // the pool changed under this epoch: queue it again
         c_.stats.epochs--;
         return true;
@@ -1598,6 +1623,10 @@ class Resolver {
         ncand = c_.h_cnt[CNT_CAND];
         if (ncand > c_.cand.cap) throw ZcError{ZC_ERR_NOMEM, "candidate buffer overflow persisted"};
       }
+      // no probe of this epoch follows: empty the tables now, on the device
+      // while the host walks (the next stream's first epoch then inserts
+      // without clearing them; later epochs clear them in their own batch)
+      clear_tables();
       if (first && (c_.flags & ZC_FLAG_TIMING)) {  // device time from the scan's end
         float ms = 0;
         HCK(hipEventElapsedTime(&ms, c_.ev1, c_.ev_meta));
@@ -3230,6 +3259,8 @@ int zc_create(zc_ctx** out, uint32_t chunk_max_size, int device, uint32_t flags)
     HCK(hipEventCreateWithFlags(&c->ev_idx, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_sha, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&c->ev_grec, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&c->ev_batch, hipEventDisableTiming));
     HCK(hipStreamCreateWithFlags(&c->sha_stream, hipStreamNonBlocking));
     HCK(hipHostMalloc((void**)&c->stage, kFeedChunk, hipHostMallocDefault));
   });
@@ -3258,6 +3289,8 @@ int zc_destroy(zc_ctx* c) {
     if (c->ev_idx) (void)hipEventDestroy(c->ev_idx);
     if (c->ev_sha) (void)hipEventDestroy(c->ev_sha);
     if (c->ev_grec) (void)hipEventDestroy(c->ev_grec);
+    if (c->ev_copy) (void)hipEventDestroy(c->ev_copy);
+    if (c->ev_batch) (void)hipEventDestroy(c->ev_batch);
     if (c->sha_stream) (void)hipStreamSynchronize(c->sha_stream);
     if (c->sha_stream) (void)hipStreamDestroy(c->sha_stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);

@@ -1064,6 +1064,20 @@ __device__ __forceinline__ void first_anchor(const uint8_t* __restrict__ data, c
   }
 }
 
+// The epoch's table inserts (zc_index_insert_kernel), also done inside the
+// metadata kernel when the tables start out empty (FusedInsert, below)
+struct FusedInsert {
+  uint64_t* ckeys;  // null: not fused
+  uint32_t cbits;
+  uint64_t* tab;  // null: no anchor table this epoch
+  uint32_t tbits;
+  uint32_t* gfilt;
+};
+__device__ __forceinline__ void class_insert(const uint64_t* __restrict__ key, uint32_t i, uint64_t* ckeys,
+                                             uint32_t cbits);
+__device__ __forceinline__ void anchor_insert(uint32_t i, uint32_t g, uint64_t fp, uint64_t* tab, uint32_t tbits,
+                                              uint32_t* __restrict__ gfilt);
+
 // zc_chunk_meta: per grid chunk i of the epoch, start = r_e + i * W: start,
 // visibility time, key, first anchor (offset, gear value, 8-byte
 // fingerprint); the chunk is not yet consumed by a match (dead = 0).  Two
@@ -1071,7 +1085,10 @@ __device__ __forceinline__ void first_anchor(const uint8_t* __restrict__ data, c
 // span digests), thread split + i searches the first anchor (a chain of
 // dependent loads), so the two latency chains overlap instead of adding up
 // (split: a multiple of the block size).  The whole grid also clears the
-// epoch's tables (no separate fills).
+// epoch's tables (no separate fills) -- or, fused (fi.ckeys; the tables are
+// empty already and every key was written before the kernel), inserts each
+// chunk into them: the key thread into the class table, the anchor thread
+// into the anchor table, in place of zc_index_insert_kernel.
 __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t n,
                                      const uint64_t* __restrict__ blk, AnchorView av, uint64_t r_e,
                                      uint32_t nchunks, uint32_t split, uint32_t W, uint64_t pw,
@@ -1079,7 +1096,7 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
                                      uint8_t* __restrict__ dead, uint64_t* __restrict__ key,
                                      uint32_t* __restrict__ cg, uint64_t* __restrict__ cfp,
                                      uint32_t* __restrict__ anc_off, uint64_t* __restrict__ hkey, uint32_t key_from,
-                                     EpochClear ec) {
+                                     EpochClear ec, FusedInsert fi) {
   ZC_URGENT();
   const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t j = gt; j < ec.cwords; j += gs) ec.ckeys[j] = ~0ull;
@@ -1104,6 +1121,7 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
       // runs): no separate copy kernel beside the index build
       if (hkey) hkey[i] = k;
     }
+    if (fi.ckeys) class_insert(key, i, fi.ckeys, fi.cbits);  // (fused: key_from == nchunks)
   } else if (gt >= split && gt - split < nchunks) {
     const uint32_t i = (uint32_t)(gt - split);
     uint32_t off, gv;
@@ -1112,6 +1130,7 @@ __global__ void zc_chunk_meta_kernel(const uint8_t* __restrict__ data, uint64_t 
     anc_off[i] = off;
     cg[i] = gv;
     cfp[i] = f;
+    if (fi.ckeys && fi.tab && off != ZC_NO_ANCHOR) anchor_insert(i, gv, f, fi.tab, fi.tbits, fi.gfilt);
   }
 }
 
@@ -1515,6 +1534,48 @@ __device__ __forceinline__ uint32_t key_slot(uint64_t k, uint32_t bits) {
   return (uint32_t)((k * kGolden) >> (64 - bits));
 }
 
+// ref i into the class table.  A ref with the same key as the ref before it
+// is not the lowest of its key: only the first ref of each run of equal keys
+// inserts (repeated content -- all-zero streams -- would otherwise serialise
+// every ref on one slot's atomics).  A slot is {high word of the key | lowest
+// ref}: one CAS inserts a new key; a ref of a key already present lowers the
+// slot's ref with a 64-bit atomicMin (equal high words: the minimum is the
+// lower ref).  key[] must be complete (the slot holder's key is read).
+__device__ __forceinline__ void class_insert(const uint64_t* __restrict__ key, uint32_t i, uint64_t* ckeys,
+                                             uint32_t cbits) {
+  if (i > 0 && key[i - 1] == key[i]) return;
+  const uint64_t k = key[i];
+  const uint64_t word = (k & 0xFFFFFFFF00000000ull) | i;  // != kEmpty: i < 2^32 - 1
+  const uint32_t mask = (1u << cbits) - 1;
+  for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
+    const unsigned long long prev =
+        atomicCAS((unsigned long long*)&ckeys[h], (unsigned long long)kEmpty, (unsigned long long)word);
+    if (prev == kEmpty) return;
+    if ((prev >> 32) == (k >> 32) && key[(uint32_t)prev] == k) {
+      atomicMin((unsigned long long*)&ckeys[h], (unsigned long long)word);
+      return;
+    }
+  }
+}
+
+// ref i (with an anchor: gear g, fingerprint fp) into the anchor table and
+// its key filter
+__device__ __forceinline__ void anchor_insert(uint32_t i, uint32_t g, uint64_t fp, uint64_t* tab, uint32_t tbits,
+                                              uint32_t* __restrict__ gfilt) {
+  const uint32_t fb = g & ((1u << kGFiltBits) - 1);
+  atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
+  const uint64_t word = ((uint64_t)i << 32) | g;
+  const uint32_t mask = (1u << tbits) - 1;
+  for (uint32_t h = table_slot(g, fp, tbits);; h = (h + 1) & mask) {
+    const unsigned long long prev =
+        atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty, (unsigned long long)word);
+    if (prev == kEmpty) {
+      tab[2 * (uint64_t)h + 1] = fp;
+      return;
+    }
+  }
+}
+
 // thread per ref: the class table (lowest ref per key) and, for a ref with an
 // anchor, the anchor table and its key filter
 __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ anc_off,
@@ -1526,30 +1587,11 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
   // anchor table: the two CAS chains run side by side
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * nref) return;
-  const bool cls_part = t < nref;
-  const uint32_t i = cls_part ? t : t - nref;
-  // a ref with the same key as the ref before it is not the lowest of its
-  // key: only the first ref of each run of equal keys inserts (repeated
-  // content -- all-zero streams -- would otherwise serialise every ref on
-  // one slot's atomics)
-  if (cls_part) {
-    // a slot is {high word of the key | lowest ref}: one CAS inserts a new
-    // key; a ref of a key already present lowers the slot's ref with a
-    // 64-bit atomicMin (equal high words: the minimum is the lower ref)
-    if (i > 0 && key[i - 1] == key[i]) return;
-    const uint64_t k = key[i];
-    const uint64_t word = (k & 0xFFFFFFFF00000000ull) | i;  // != kEmpty: i < 2^32 - 1
-    const uint32_t mask = (1u << cbits) - 1;
-    for (uint32_t h = key_slot(k, cbits);; h = (h + 1) & mask) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)&ckeys[h], (unsigned long long)kEmpty,
-                                                (unsigned long long)word);
-      if (prev == kEmpty) return;
-      if ((prev >> 32) == (k >> 32) && key[(uint32_t)prev] == k) {
-        atomicMin((unsigned long long*)&ckeys[h], (unsigned long long)word);
-        return;
-      }
-    }
+  if (t < nref) {
+    class_insert(key, t, ckeys, cbits);
+    return;
   }
+  const uint32_t i = t - nref;
   if (!tab) return;
   // every ref with an anchor enters the anchor table (the probe keeps class
   // leaders only: classes are not known yet); the ref's three words are read
@@ -1557,18 +1599,7 @@ __global__ void zc_index_insert_kernel(const uint64_t* __restrict__ key, const u
   const uint32_t ao = anc_off[i], g = cg[i];
   const uint64_t fpi = cfp[i];
   if (ao == ZC_NO_ANCHOR) return;
-  const uint32_t fb = g & ((1u << kGFiltBits) - 1);
-  atomicOr(&gfilt[fb >> 5], 1u << (fb & 31));
-  const uint64_t word = ((uint64_t)i << 32) | g;
-  const uint32_t mask = (1u << tbits) - 1;
-  for (uint32_t h = table_slot(g, fpi, tbits);; h = (h + 1) & mask) {
-    const unsigned long long prev = atomicCAS((unsigned long long*)&tab[2 * (uint64_t)h], (unsigned long long)kEmpty,
-                                              (unsigned long long)word);
-    if (prev == kEmpty) {
-      tab[2 * (uint64_t)h + 1] = fpi;
-      return;
-    }
-  }
+  anchor_insert(i, g, fpi, tab, tbits, gfilt);
 }
 
 // historic index: entries [e0, e0 + cnt) that have an anchor into its table
@@ -3062,9 +3093,12 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
                               uint32_t nconf, uint32_t nsref, uint32_t W, uint64_t pw, const EpochIndex& ix,
                               hipStream_t s, hipEvent_t after_meta) {
   const uint32_t nref = nconf + nsref;
-  const EpochClear ec{ix.ckeys, nref ? 1u << ix.cbits : 0u, ix.tab,
-                      ix.tab ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab ? kGFiltWords : 0u, ix.counters,
-                      ix.scnt, ix.h_scnt};
+  // fused: the tables are empty and every key is in (the scan wrote them)
+  const bool fused = ix.tables_clean && nconf == 0 && nsref && ix.key_from == nsref;
+  const EpochClear ec{ix.ckeys, nref && !fused ? 1u << ix.cbits : 0u, ix.tab,
+                      ix.tab && !fused ? 2ull << ix.tbits : 0ull, ix.gfilt, ix.tab && !fused ? kGFiltWords : 0u,
+                      ix.counters, ix.scnt, ix.h_scnt};
+  const FusedInsert fi{fused ? ix.ckeys : nullptr, ix.cbits, ix.tab, ix.tbits, ix.gfilt};
   // enough threads for the grid chunks, and for the clears at a few words each
   const uint64_t words = (uint64_t)ec.cwords + ec.twords + ec.gwords;
   const uint32_t split = (uint32_t)(blocks_for(nsref, 128) * 128);  // the anchor threads' first
@@ -3072,14 +3106,15 @@ hipError_t launch_epoch_index(const uint8_t* data, uint64_t n, const uint64_t* b
       std::max<uint64_t>({(uint64_t)split + nsref, std::min<uint64_t>(words / 4, 1u << 20), CNT_LAST});
   hipLaunchKernelGGL(zc_chunk_meta_kernel, dim3(blocks_for(threads, 128)), dim3(128), 0, s, data, n, blk, av, r_e,
                      nsref, split, W, pw, ix.start + nconf, ix.vis + nconf, ix.dead + nconf, ix.key + nconf,
-                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ix.hkey, ix.key_from, ec);
+                     ix.cg + nconf, ix.cfp + nconf, ix.anc + nconf, ix.hkey, ix.key_from, ec, fi);
   if (after_meta) {
     const hipError_t e = hipEventRecord(after_meta, s);
     if (e != hipSuccess) return e;
   }
   if (!nref) return hipGetLastError();
-  hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc, ix.cg,
-                     ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
+  if (!fused)
+    hipLaunchKernelGGL(zc_index_insert_kernel, dim3(blocks_for(2ull * nref, 256)), dim3(256), 0, s, ix.key, ix.anc,
+                       ix.cg, ix.cfp, nref, ix.ckeys, ix.cbits, ix.tab, ix.tbits, ix.gfilt);
   hipLaunchKernelGGL(zc_class_lead_kernel, dim3(blocks_for(nref, 256)), dim3(256), 0, s, ix.key, ix.anc, nref,
                      ix.ckeys, ix.cbits, ix.cls, ix.ancless, ix.pairs, ix.counters,
                      ShaGrid{ix.gsha, ix.gsha ? ix.n_gsha : 0, n, W}, ix.start);
@@ -3099,6 +3134,27 @@ hipError_t launch_class_sha(const uint8_t* gsha, uint64_t n_gsha, uint64_t n, ui
 }
 
 uint32_t probe_filter_words() { return kGFiltWords; }
+
+// 16-byte stores over the three tables (each a whole number of 16-byte units)
+__global__ void zc_tables_clear_kernel(uint4* __restrict__ ckeys, uint64_t cq, uint4* __restrict__ tab, uint64_t tq,
+                                       uint4* __restrict__ gfilt, uint64_t gq) {
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+  const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u), zero = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t j = gt; j < cq; j += gs) ckeys[j] = ones;
+  for (uint64_t j = gt; j < tq; j += gs) tab[j] = ones;
+  for (uint64_t j = gt; j < gq; j += gs) gfilt[j] = zero;
+}
+
+hipError_t launch_tables_clear(uint64_t* ckeys, uint64_t cwords, uint64_t* tab, uint64_t twords, uint32_t* gfilt,
+                               uint64_t gwords, hipStream_t s) {
+  if ((cwords | twords) % 2 || gwords % 4) return hipErrorInvalidValue;
+  const uint64_t cq = cwords / 2, tq = twords / 2, gq = gwords / 4;
+  if (!(cq + tq + gq)) return hipSuccess;
+  const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(std::max({cq, tq, gq}), 256), 2048);
+  hipLaunchKernelGGL(zc_tables_clear_kernel, dim3(blocks), dim3(256), 0, s, (uint4*)ckeys, cq, (uint4*)tab, tq,
+                     (uint4*)gfilt, gq);
+  return hipGetLastError();
+}
 
 hipError_t launch_ref_meta(const uint8_t* data, const uint64_t* blk, AnchorView av, const uint64_t* starts,
                            uint32_t cnt, uint32_t W, uint64_t pw, uint64_t* key, uint32_t* anc_off, uint32_t* cg,
