@@ -3138,6 +3138,9 @@ uint32_t probe_filter_words() { return kGFiltWords; }
 // 16-byte stores over the three tables (each a whole number of 16-byte units)
 __global__ void zc_tables_clear_kernel(uint4* __restrict__ ckeys, uint64_t cq, uint4* __restrict__ tab, uint64_t tq,
                                        uint4* __restrict__ gfilt, uint64_t gq) {
+  // (urgent: it runs beside the grid SHA-1, and the historic registration
+  // queued behind it waits for it; at normal priority it took 0.1-1.8 ms there)
+  ZC_URGENT();
   const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
   const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u), zero = make_uint4(0u, 0u, 0u, 0u);
   for (uint64_t j = gt; j < cq; j += gs) ckeys[j] = ones;
