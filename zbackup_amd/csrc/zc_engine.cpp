@@ -1625,8 +1625,11 @@ class Resolver {
       }
       // no probe of this epoch follows: empty the tables now, on the device
       // while the host walks (the next stream's first epoch then inserts
-      // without clearing them; later epochs clear them in their own batch)
-      clear_tables();
+      // without clearing them; later epochs clear them in their own batch).
+      // Not beside the grid SHA-1 (ZC_FLAG_SHA1): there the clear delayed
+      // the historic registration queued behind it (hist_ms 0.26 -> 1-2.8 ms,
+      // profiles/r06_sha1_clear_ab.txt); run_final clears after the SHA-1.
+      if (!(c_.flags & ZC_FLAG_SHA1)) clear_tables();
       if (first && (c_.flags & ZC_FLAG_TIMING)) {  // device time from the scan's end
         float ms = 0;
         HCK(hipEventElapsedTime(&ms, c_.ev1, c_.ev_meta));
